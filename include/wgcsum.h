@@ -1,0 +1,164 @@
+/*
+ * wgcsum.h -- C ABI of the MI355X-native (gfx950) Internet-checksum hot path
+ * of muhtutorials/wireguard's `tun` package.
+ *
+ * Plain C types only (pointers and sizes); no torch, no HIP types in the
+ * signatures (streams are passed as `void*` = hipStream_t, NULL = the
+ * context's own stream).  Every entry point is thread-safe: calls on one
+ * context are serialized by a context mutex (the reference serializes Read
+ * with Tun.readMu and Write with Tun.writeMu, tun/tun.go:101,:105).
+ *
+ * Reference interfaces replaced (file:line in /root/reference):
+ *   wgcs_checksum_batch       batch form of checksum()            tun/checksum.go:152-167
+ *                             + checksumValid()                   tun/gro.go:554-612
+ *                             + gsoSplit's per-segment L4 sum      tun/gro.go:1469-1488
+ *                             + gsoNoneChecksum()                 tun/gro.go:1497-1517
+ *                             + IPv4 header checksum sites        tun/gro.go:1134-1138,1217-1221,1434-1436
+ *   wgcs_checksum             checksum(b, initial)                tun/checksum.go:152-167
+ *   wgcs_checksum_valid       checksumValid(pkt, iphLen, proto, isV6)  tun/gro.go:554-612
+ *   wgcs_gso_none_checksum    gsoNoneChecksum(readBuf, start, off)     tun/gro.go:1497-1517
+ *   wgcs_gso_split            gsoSplit(readBuf, hdr, bufs, sizes, offset, isV6)  tun/gro.go:1373-1493
+ *   wgcs_gso_split_batch      device-resident batch of gsoSplit calls  (one per Tun.Read)
+ *   wgcs_handle_virtio_read   handleVirtioRead(readBuf, bufs, sizes, offset)  tun/tun.go:514-632
+ *   wgcs_handle_gro           handleGRO(bufs, offset, tcpTable, udpTable, canUDPGRO, &toWrite)
+ *                                                                 tun/gro.go:1326-1367
+ * Status codes map 1:1 onto the reference's Go errors (see WGCS_ERR_*).
+ */
+#ifndef WGCSUM_H
+#define WGCSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WGCS_ABI_VERSION 1
+
+/* ---- status codes (negative); Go sentinel / error each one maps to ---- */
+#define WGCS_OK 0
+#define WGCS_ERR_INVALID_ARG (-1)       /* API misuse (NULL ctx, n too large, ...) */
+#define WGCS_ERR_SHORT_BUFFER (-2)      /* io.ErrShortBuffer                 gro.go:75,86 */
+#define WGCS_ERR_TOO_MANY_SEGMENTS (-3) /* tun.ErrTooManySegments            tun.go:30, gro.go:1410 */
+#define WGCS_ERR_INVALID_OFFSET (-4)    /* errors.New("invalid offset")     gro.go:1336 */
+#define WGCS_ERR_UNSUPPORTED_GSO (-5)   /* "unsupported virtio GSO type: %d" tun.go:567 */
+#define WGCS_ERR_IP_GSO_MISMATCH (-6)   /* "IP header version: %d, GSO type: %d" tun.go:575,584 */
+#define WGCS_ERR_BAD_IP_VERSION (-7)    /* "invalid IP header version: %d"  tun.go:591 */
+#define WGCS_ERR_PACKET_TOO_SHORT (-8)  /* "packet is too short"            tun.go:603 */
+#define WGCS_ERR_TCP_HDR_LEN (-9)       /* "TCP header length is invalid: %d" tun.go:611 */
+#define WGCS_ERR_HDR_LEN (-10)          /* "length of packet (%d) < virtioNetHdr.hdrLen (%d)" tun.go:616 */
+#define WGCS_ERR_CSUM_OFFSET (-11)      /* "end of checksum offset (%d) exceeds packet length (%d)" tun.go:625 */
+#define WGCS_ERR_READ_OVERFLOW (-12)    /* "read length %d overflows bufs element length %d" tun.go:546 */
+#define WGCS_ERR_OUT_OF_RANGE (-13)     /* input on which the Go code would panic (slice bounds) */
+#define WGCS_ERR_HIP (-100)             /* HIP runtime error (message: wgcs_last_error) */
+#define WGCS_ERR_NOMEM (-101)
+#define WGCS_ERR_NO_DEVICE (-102)
+
+/* ---- batch descriptor: one packet (or byte range) in a device arena ---- */
+typedef struct wgcs_pkt {
+  uint64_t off;        /* byte offset of the packet (IP header) in the arena      */
+  uint32_t len;        /* packet length in bytes (< 2^31)                           */
+  uint16_t csum_start; /* L4 start = IP header length (iphLen / virtio csumStart)   */
+  uint8_t csum_offset; /* checksum field offset from csum_start (16 TCP, 6 UDP)     */
+  uint8_t flags;       /* WGCS_PKT_*                                                */
+} wgcs_pkt;          /* 16 bytes */
+
+#define WGCS_PKT_V6 0x01  /* addresses at 8/24 (16 B) instead of 12/16 (4 B)         */
+#define WGCS_PKT_UDP 0x02 /* pseudo-header protocol 17 instead of 6                   */
+
+/* ---- batch modes (out element: u16, except VALIDATE: u8 0/1) ---- */
+#define WGCS_MODE_FOLD 0     /* out = checksum(pkt[0:len], initial[i])                 checksum.go:152 */
+#define WGCS_MODE_L4_FILL 1  /* out = ^checksum(pkt[cs:len] with field zeroed,
+                                pseudoHeaderChecksumNoFold(src,dst,proto,len-cs))     gro.go:1469-1488 */
+#define WGCS_MODE_VALIDATE 2 /* out = checksumValid(pkt, cs, proto, isV6)             gro.go:554-612 */
+#define WGCS_MODE_PARTIAL 3  /* out = ^checksum(pkt[cs:len] field zeroed, BE16(field)) gro.go:1497-1517 */
+#define WGCS_MODE_IP4HDR 4   /* out = ^checksum(pkt[0:cs] with [10:12] zeroed, 0)      gro.go:1134-1138 */
+
+#define WGCS_F_INPLACE 0x1 /* also store the result big-endian into the packet's field */
+
+typedef struct wgcs_ctx wgcs_ctx;
+
+/* virtioNetHdr, tun/gro.go:42-67 (10 bytes on the wire, native byte order) */
+typedef struct wgcs_virtio_hdr {
+  uint8_t flags;
+  uint8_t gso_type;
+  uint16_t hdr_len;
+  uint16_t gso_size;
+  uint16_t csum_start;
+  uint16_t csum_offset;
+} wgcs_virtio_hdr;
+
+/* one job of wgcs_gso_split_batch: a Tun.Read super-packet */
+typedef struct wgcs_gso_job {
+  uint64_t off;   /* offset of the 10-byte virtio header in the device arena */
+  uint32_t len;   /* bytes read from the TUN fd (virtio header included)     */
+  uint32_t flags; /* WGCS_GSO_JOB_*                                          */
+} wgcs_gso_job;
+
+/* default (0): handleVirtioRead semantics -- validate the header, recompute
+ * hdrLen, GSO_NONE copy (+ gsoNoneChecksum), tun/tun.go:514-632.
+ * RAW: gsoSplit(readBuf, hdr, ...) semantics with the header fields taken as
+ * given (gro.go:1373-1493); WGCS_GSO_JOB_V6 then gives isV6. */
+#define WGCS_GSO_JOB_RAW 0x1u
+#define WGCS_GSO_JOB_V6 0x2u
+
+/* ---- lifecycle / diagnostics ---- */
+int wgcs_abi_version(void);
+int wgcs_device_count(int *count);
+int wgcs_init(int device, wgcs_ctx **out);
+int wgcs_destroy(wgcs_ctx *ctx);
+const char *wgcs_strerror(int status);
+const char *wgcs_last_error(wgcs_ctx *ctx);
+int wgcs_sync(wgcs_ctx *ctx);
+/* CU count of the context's device (grid sizing, reporting) */
+int wgcs_num_cu(wgcs_ctx *ctx);
+
+/* ---- device-resident batch entry points (HBM in, HBM out; async on stream) ----
+ * The arena must be readable through align_up(off+len, 16) for every packet
+ * (always true for hipMalloc / torch allocations, which are page-granular). */
+int wgcs_checksum_batch(wgcs_ctx *ctx, int mode, unsigned flags, uint8_t *d_arena,
+                        const wgcs_pkt *d_pkts, const uint64_t *d_initial, uint32_t n,
+                        void *d_out, void *stream);
+
+/* gsoSplit for n_jobs super-packets.  Job j writes its segments into output
+ * slots [j*max_segs, (j+1)*max_segs), slot s at d_out + s*out_stride + offset
+ * (like bufs[s][offset:]).  d_sizes[slot] = packet size; d_count[j] = the
+ * return value n (>= 0) and d_status[j] = 0 or a WGCS_ERR_* code, with the
+ * reference's ErrTooManySegments semantics (n = max_segs-1, gro.go:1409-1410).
+ * Includes handleVirtioRead's GSO validation (tun/tun.go:557-631). */
+int wgcs_gso_split_batch(wgcs_ctx *ctx, const uint8_t *d_arena, const wgcs_gso_job *d_jobs,
+                         uint32_t n_jobs, uint8_t *d_out, uint32_t out_stride, uint32_t offset,
+                         uint32_t max_segs, int32_t *d_sizes, int32_t *d_count,
+                         int32_t *d_status, void *stream);
+
+/* ---- reference-shaped entry points on host buffers (Go-call granularity) ----
+ * These stage through the context's pinned ring, run the HIP kernels and copy
+ * results back; they keep the reference's argument meaning and errors. */
+int wgcs_checksum(wgcs_ctx *ctx, const uint8_t *b, size_t n, uint64_t initial, uint16_t *out);
+int wgcs_checksum_valid(wgcs_ctx *ctx, const uint8_t *pkt, size_t len, uint8_t iph_len,
+                        uint8_t proto, int is_v6, int *valid);
+int wgcs_gso_none_checksum(wgcs_ctx *ctx, uint8_t *read_buf, size_t len, uint16_t csum_start,
+                           uint16_t csum_offset);
+/* host batch: same semantics as wgcs_checksum_batch on a host arena */
+int wgcs_checksum_batch_host(wgcs_ctx *ctx, int mode, unsigned flags, uint8_t *h_arena,
+                             size_t arena_len, const wgcs_pkt *h_pkts, const uint64_t *h_initial,
+                             uint32_t n, void *h_out);
+/* bufs[i] points at a buffer of buf_lens[i] bytes; sizes[] receives packet sizes. */
+int wgcs_gso_split(wgcs_ctx *ctx, uint8_t *read_buf, size_t len, const wgcs_virtio_hdr *hdr,
+                   uint8_t *const *bufs, const size_t *buf_lens, int nbufs, int *sizes,
+                   int offset, int is_v6, int *n_out);
+/* read_buf: the bytes read from the TUN fd, virtio header first (tun/tun.go:490). */
+int wgcs_handle_virtio_read(wgcs_ctx *ctx, uint8_t *read_buf, size_t n, uint8_t *const *bufs,
+                            const size_t *buf_lens, int nbufs, int *sizes, int offset,
+                            int *n_out);
+/* Go-slice form of handleGRO: lens[i] = len(bufs[i]), caps[i] = cap(bufs[i]).
+ * bufs/lens/caps are updated in place (appends grow lens[i]; prepends swap
+ * entries, gro.go:696-697); to_write receives the indices to write. */
+int wgcs_handle_gro(wgcs_ctx *ctx, uint8_t **bufs, size_t *lens, size_t *caps, int n,
+                    int offset, int can_udp_gro, int *to_write, int *n_to_write);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WGCSUM_H */

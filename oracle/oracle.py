@@ -1,0 +1,164 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes wrapper around oracle/_build/libwgoracle.so.
+
+The oracle is the CPU restatement of the reference's hot path
+(/root/reference/tun/checksum.go, tun/gro.go, tun/tun.go:514-632), see
+wg_oracle.c.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg may import this module; the product (wireguard_amd/) never does.
+
+Parity pinning: the reference ships no tests or fixtures and cannot be built
+here (no Go toolchain), so the restatement is pinned by independent KATs and a
+closed-form cross-check only ("parity unpinned" against reference outputs; see
+DESIGN.md).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "libwgoracle.so")
+
+PKT_DTYPE = np.dtype(
+    [("off", "<u8"), ("len", "<u4"), ("csum_start", "<u2"), ("csum_offset", "u1"), ("flags", "u1")]
+)
+assert PKT_DTYPE.itemsize == 16
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _SO
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = C.CDLL(_SO)
+        u8p = C.POINTER(C.c_uint8)
+        L.or_checksum_nofold.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
+        L.or_checksum_nofold.restype = C.c_uint64
+        L.or_checksum.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
+        L.or_checksum.restype = C.c_uint16
+        L.or_pseudo_header_nofold.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint8, C.c_uint16]
+        L.or_pseudo_header_nofold.restype = C.c_uint64
+        L.or_checksum_valid.argtypes = [C.c_void_p, C.c_size_t, C.c_uint8, C.c_uint8, C.c_int]
+        L.or_checksum_valid.restype = C.c_int
+        L.or_gso_none_checksum.argtypes = [C.c_void_p, C.c_size_t, C.c_uint16, C.c_uint16]
+        L.or_gso_none_checksum.restype = C.c_int
+        L.or_handle_virtio_read.argtypes = [
+            C.c_void_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.c_int,
+            C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_int),
+        ]
+        L.or_handle_virtio_read.restype = C.c_int
+        L.or_handle_gro.argtypes = [
+            C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.c_int, C.c_int, C.c_int,
+            C.POINTER(C.c_int), C.POINTER(C.c_int),
+        ]
+        L.or_handle_gro.restype = C.c_int
+        L.or_checksum_batch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int]
+        L.or_checksum_batch.restype = None
+        L.or_checksum_batch_mt.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int]
+        L.or_checksum_batch_mt.restype = None
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def checksum_nofold(b: bytes, initial: int = 0) -> int:
+    a = np.frombuffer(bytes(b) + b"\0", dtype=np.uint8)
+    return lib().or_checksum_nofold(_ptr(a), len(b), initial & (2**64 - 1))
+
+
+def checksum(b: bytes, initial: int = 0) -> int:
+    a = np.frombuffer(bytes(b) + b"\0", dtype=np.uint8)
+    return lib().or_checksum(_ptr(a), len(b), initial & (2**64 - 1))
+
+
+def pseudo_header_nofold(src: bytes, dst: bytes, proto: int, total_len: int) -> int:
+    s = np.frombuffer(bytes(src), dtype=np.uint8)
+    d = np.frombuffer(bytes(dst), dtype=np.uint8)
+    return lib().or_pseudo_header_nofold(_ptr(s), _ptr(d), len(src), proto, total_len & 0xFFFF)
+
+
+def checksum_valid(pkt: bytes, iph_len: int, proto: int, is_v6: bool) -> bool:
+    a = np.frombuffer(bytes(pkt) + b"\0", dtype=np.uint8)
+    return bool(lib().or_checksum_valid(_ptr(a), len(pkt), iph_len, proto, int(is_v6)))
+
+
+def checksum_batch(mode: int, arena: np.ndarray, pkts: np.ndarray, initial=None, inplace=False):
+    """Run the oracle's batch restatement; returns the per-packet outputs."""
+    assert arena.dtype == np.uint8 and pkts.dtype == PKT_DTYPE
+    n = len(pkts)
+    out = np.zeros(n, dtype=np.uint8 if mode == 2 else np.uint16)
+    ini = 0
+    if initial is not None:
+        initial = np.ascontiguousarray(initial, dtype=np.uint64)
+        ini = _ptr(initial)
+    lib().or_checksum_batch(mode, _ptr(arena), _ptr(pkts), ini or None, n, _ptr(out), int(inplace))
+    return out
+
+
+def checksum_batch_mt(mode: int, arena: np.ndarray, pkts: np.ndarray, threads: int):
+    n = len(pkts)
+    out = np.zeros(n, dtype=np.uint8 if mode == 2 else np.uint16)
+    lib().or_checksum_batch_mt(mode, _ptr(arena), _ptr(pkts), n, _ptr(out), threads)
+    return out
+
+
+def _bufs_ctypes(bufs):
+    u8p = C.POINTER(C.c_uint8)
+    arr = (u8p * len(bufs))()
+    for i, b in enumerate(bufs):
+        arr[i] = C.cast(b.ctypes.data, u8p)
+    return arr
+
+
+def handle_virtio_read(read_buf: bytearray, bufs: list, offset: int):
+    """Oracle handleVirtioRead.  Mutates read_buf (like the reference) and the
+    numpy bufs.  Returns (rc, n, sizes)."""
+    rb = np.frombuffer(read_buf, dtype=np.uint8) if not isinstance(read_buf, np.ndarray) else read_buf
+    lens = (C.c_size_t * len(bufs))(*[len(b) for b in bufs])
+    sizes = (C.c_int * len(bufs))()
+    n = C.c_int(0)
+    rc = lib().or_handle_virtio_read(_ptr(rb), len(rb), _bufs_ctypes(bufs), lens, len(bufs), sizes, offset, C.byref(n))
+    return rc, n.value, list(sizes)
+
+
+def handle_gro(bufs: list, lens: list, offset: int, can_udp_gro: bool):
+    """Oracle handleGRO.  bufs: list of numpy uint8 arrays (capacity = len(array)),
+    lens: slice lengths.  Returns (rc, to_write, order, lens) where `order[i]` is
+    the index of the original numpy buffer now at position i (prepends swap)."""
+    n = len(bufs)
+    u8p = C.POINTER(C.c_uint8)
+    arr = _bufs_ctypes(bufs)
+    orig = [C.cast(arr[i], C.c_void_p).value for i in range(n)]
+    clens = (C.c_size_t * n)(*lens)
+    ccaps = (C.c_size_t * n)(*[len(b) for b in bufs])
+    tw = (C.c_int * n)()
+    ntw = C.c_int(0)
+    rc = lib().or_handle_gro(arr, clens, ccaps, n, offset, int(can_udp_gro), tw, C.byref(ntw))
+    order = [orig.index(C.cast(arr[i], C.c_void_p).value) for i in range(n)]
+    return rc, list(tw)[: ntw.value], order, list(clens)
+
+
+# ---------------------------------------------------------------------------
+# Independent closed form: checksum(b, init) ==
+#   S == 0 ? 0 : 1 + (S - 1) mod 0xFFFF,  S = sum of big-endian u16 words
+#   (odd tail zero-padded) + init, as a plain integer.
+# ---------------------------------------------------------------------------
+def closed_form_checksum(b: bytes, initial: int = 0) -> int:
+    b = bytes(b)
+    if len(b) % 2:
+        b += b"\0"
+    s = int(np.frombuffer(b, dtype=">u2").astype(np.uint64).sum()) + initial
+    return 0 if s == 0 else 1 + (s - 1) % 0xFFFF

@@ -1,0 +1,42 @@
+#!/bin/bash
+# Run GPU steps on the gpurun box.  Each step has its own time limit; a test
+# failure does not stop the chain, but a timeout / abort / segfault does (no
+# further GPU work after a fault).  Logs go under gpurun_out/.
+# usage: scripts/gpu_steps.sh STEP...   STEP = tests | bench | prof | pmc | smoke
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+TAG=${TAG:-r1}
+step() {
+  local name=$1 lim=$2; shift 2
+  echo "== [$name] $(date +%T) $*"
+  timeout -k 10 "$lim" "$@" > "$OUT/$TAG.$name.log" 2>&1
+  local rc=$?
+  echo "== [$name] rc=$rc"
+  tail -n 5 "$OUT/$TAG.$name.log"
+  case $rc in 124|134|137|139) echo "FATAL in $name (rc=$rc): stopping"; exit $rc;; esac
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    tests) step tests 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests-all) step tests 1100 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    sweep) step sweep 400 python scripts/sweep_checksum.py ;;
+    sweep-cfg3) step sweep_cfg3 400 python scripts/sweep_checksum.py --config cfg3 ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 400 python bench.py --steps 200 --warmup 20 ;;
+    bench-noevt) step bench_noevt 300 python bench.py --steps 200 --warmup 20 --no-event-timing --cpu-seconds 0 ;;
+    bench-fill) step bench_fill 300 python bench.py --steps 200 --warmup 20 --mode fill --cpu-seconds 0 ;;
+    bench-cfg3) step bench_cfg3 300 python bench.py --config cfg3 --steps 100 --warmup 10 --cpu-seconds 0 ;;
+    bench-cfg4) step bench_cfg4 300 python bench.py --config cfg4 --steps 100 --warmup 10 --cpu-seconds 0 ;;
+    bench-cfg5) step bench_cfg5 300 python bench.py --config cfg5 --steps 100 --warmup 10 --cpu-seconds 0 ;;
+    prof) (cd /tmp && step prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0) ;;
+    pmc) (cd /tmp && step pmc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-event-timing) ;;
+    pmc-w) (cd /tmp && step pmcw 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-event-timing) ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== done"

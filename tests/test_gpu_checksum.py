@@ -1,0 +1,176 @@
+"""GPU parity: the gfx950 checksum kernels vs the oracle (CPU restatement of
+/root/reference/tun/checksum.go + gro.go), bit-exact, through the C ABI."""
+import numpy as np
+import pytest
+
+import oracle
+from wireguard_amd import synth
+from wireguard_amd.tun import (MODE_FOLD, MODE_IP4HDR, MODE_L4_FILL, MODE_PARTIAL, MODE_VALIDATE, PKT_DTYPE, PKT_UDP,
+                               PKT_V6)
+
+pytestmark = pytest.mark.gpu
+
+INITS = [0, 0xFFFF, 2**64 - 1, 1, 0x1234567890ABCDEF, 0xFFFF0000FFFF0000]
+
+
+def _pkts(offs, lens, cs=0, co=0, flags=0):
+    p = np.zeros(len(offs), dtype=PKT_DTYPE)
+    p["off"] = offs
+    p["len"] = lens
+    p["csum_start"] = cs
+    p["csum_offset"] = co
+    p["flags"] = flags
+    return p
+
+
+def _both(dev, mode, arena, pkts, initial=None, inplace=False):
+    a_gpu = arena.copy()
+    a_cpu = arena.copy()
+    got = dev.checksum_batch_host(mode, a_gpu, pkts, initial=initial, inplace=inplace)
+    want = oracle.checksum_batch(mode, a_cpu, pkts, initial=initial, inplace=inplace)
+    return got, want, a_gpu, a_cpu
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_fold_all_small_lengths_random_alignment(dev, seed):
+    rng = np.random.default_rng(seed)
+    arena = rng.integers(0, 256, size=1 << 18, dtype=np.uint8)
+    lens = np.tile(np.arange(0, 301), 4)
+    offs = rng.integers(0, len(arena) - 400, size=len(lens))
+    init = rng.choice(np.array(INITS, dtype=np.uint64), size=len(lens))
+    init[::7] = rng.integers(0, 2**63, size=len(init[::7]), dtype=np.uint64) * 2 + 1
+    got, want, _, _ = _both(dev, MODE_FOLD, arena, _pkts(offs, lens), initial=init)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("fill", [0x00, 0xFF])
+def test_fold_constant_arenas(dev, fill):
+    arena = np.full(1 << 17, fill, dtype=np.uint8)
+    lens = np.concatenate([np.arange(0, 200), [1023, 1024, 1025, 4096, 9000, 65535]])
+    rng = np.random.default_rng(7)
+    offs = rng.integers(0, len(arena) - 65536, size=len(lens))
+    for ini in INITS:
+        init = np.full(len(lens), ini, dtype=np.uint64)
+        got, want, _, _ = _both(dev, MODE_FOLD, arena, _pkts(offs, lens), initial=init)
+        assert np.array_equal(got, want), f"init={ini:#x}"
+    if fill == 0:
+        # S == 0 -> 0x0000 must stay distinct from S ≡ 0 (mod 0xFFFF) -> 0xFFFF
+        got = dev.checksum_batch_host(MODE_FOLD, arena, _pkts(offs, lens))
+        assert (got == 0).all()
+
+
+def test_fold_large_lengths(dev):
+    rng = np.random.default_rng(11)
+    arena = rng.integers(0, 256, size=1 << 21, dtype=np.uint8)
+    lens = rng.integers(0, 65536, size=300)
+    lens[:4] = [65535, 65534, 8191, 8193]
+    offs = rng.integers(0, len(arena) - 65536, size=len(lens))
+    init = rng.integers(0, 2**64 - 1, size=len(lens), dtype=np.uint64)
+    got, want, _, _ = _both(dev, MODE_FOLD, arena, _pkts(offs, lens), initial=init)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("kinds", ["tcp4", "udp4", "tcp6", "udp6", "mixed"])
+@pytest.mark.parametrize("frame_len,stride", [(1500, None), (1501, 1509), (64, 67), (9000, 9003), (48, None)])
+@pytest.mark.parametrize("valid", [True, False])
+def test_validate_and_fill_synth(dev, kinds, frame_len, stride, valid):
+    if frame_len < 60 and kinds in ("tcp6", "mixed"):
+        pytest.skip("IPv6/TCP needs 60 bytes")
+    arena, pkts, _ = synth.make_batch(512, frame_len, kinds=kinds, stride=stride, valid=valid, seed=frame_len)
+    got, want, _, _ = _both(dev, MODE_VALIDATE, arena, pkts)
+    assert np.array_equal(got, want)
+    assert bool(got.all()) == valid and bool(got.any()) == valid
+    got, want, _, _ = _both(dev, MODE_L4_FILL, arena, pkts)
+    assert np.array_equal(got, want)
+    got, want, ag, ac = _both(dev, MODE_L4_FILL, arena, pkts, inplace=True)
+    assert np.array_equal(got, want) and np.array_equal(ag, ac)
+
+
+def test_validate_random_descriptors(dev):
+    """Arbitrary (even odd) csum_start / lengths / alignment on random bytes."""
+    rng = np.random.default_rng(5)
+    arena = rng.integers(0, 256, size=1 << 20, dtype=np.uint8)
+    n = 4000
+    flags = rng.integers(0, 4, size=n)
+    lens = rng.integers(40, 3000, size=n)
+    cs = np.minimum(rng.integers(0, 80, size=n), lens - 20)
+    cs[::3] = np.where(flags[::3] & 1, 40, 20)
+    offs = np.arange(n) * 3003 + rng.integers(0, 3, size=n)  # disjoint packets, odd alignments
+    arena = rng.integers(0, 256, size=n * 3003 + 64, dtype=np.uint8)
+    p = _pkts(offs, lens, cs, 0, flags)
+    got, want, _, _ = _both(dev, MODE_VALIDATE, arena, p)
+    assert np.array_equal(got, want)
+    co = np.where(flags & PKT_UDP, 6, 16)
+    ok = cs + co + 2 <= lens
+    p = _pkts(offs[ok], lens[ok], cs[ok], co[ok], flags[ok])
+    got, want, _, _ = _both(dev, MODE_L4_FILL, arena, p)
+    assert np.array_equal(got, want)
+    # force a valid checksum into every packet and validate
+    _, _, filled, _ = _both(dev, MODE_L4_FILL, arena, p, inplace=True)
+    v = dev.checksum_batch_host(MODE_VALIDATE, filled, p)
+    assert np.array_equal(v, oracle.checksum_batch(MODE_VALIDATE, filled, p))
+    even = (p["csum_start"] % 2 == 0) & (p["csum_start"] >= np.where(p["flags"] & PKT_V6, 40, 20))
+    assert v[even].all()
+
+
+def test_partial_gso_none(dev):
+    rng = np.random.default_rng(9)
+    n = 600
+    lens = rng.integers(2, 4000, size=n)
+    cs = rng.integers(0, 200, size=n) % lens
+    co = rng.integers(0, 256, size=n)
+    ok = cs + co + 2 <= lens
+    lens, cs, co = lens[ok], cs[ok], co[ok]
+    m = len(lens)
+    arena = rng.integers(0, 256, size=m * 4003 + 64, dtype=np.uint8)
+    p = _pkts(np.arange(m) * 4003 + rng.integers(0, 3, size=m), lens, cs, co)  # disjoint, odd alignments
+    got, want, ag, ac = _both(dev, MODE_PARTIAL, arena, p, inplace=True)
+    assert np.array_equal(got, want) and np.array_equal(ag, ac)
+    got, want, _, _ = _both(dev, MODE_PARTIAL, arena, p)
+    assert np.array_equal(got, want)
+
+
+def test_partial_all_zero_is_zero_not_ffff(dev):
+    arena = np.zeros(4096, dtype=np.uint8)
+    p = _pkts([1, 100, 1001], [1000, 37, 3], [10, 3, 0], [6, 16, 1])
+    got, want, _, _ = _both(dev, MODE_PARTIAL, arena, p)
+    assert np.array_equal(got, want) and (got == 0xFFFF).all()  # ^checksum(zeros, 0) = ^0
+
+
+def test_ip4hdr(dev):
+    arena, pkts, _ = synth.make_batch(1000, 1500, kinds="tcp4", stride=1503)
+    rng = np.random.default_rng(3)
+    pkts["csum_start"] = rng.integers(5, 16, size=len(pkts)) * 4
+    got, want, ag, ac = _both(dev, MODE_IP4HDR, arena, pkts, inplace=True)
+    assert np.array_equal(got, want) and np.array_equal(ag, ac)
+    arena2, pkts2, _ = synth.make_batch(1000, 1500, kinds="tcp4", stride=1501)
+    got = dev.checksum_batch_host(MODE_IP4HDR, arena2, pkts2)
+    a = arena2[: 1000 * 1501].reshape(1000, 1501)
+    stored = (a[:, 10].astype(np.uint16) << 8) | a[:, 11]
+    assert np.array_equal(got, stored)  # synth wrote valid header checksums
+
+
+def test_reference_shaped_single_calls(dev):
+    rng = np.random.default_rng(2)
+    # RFC 1071 §3 example
+    assert dev.checksum(bytes([0x00, 0x01, 0xF2, 0x03, 0xF4, 0xF5, 0xF6, 0xF7]), 0) == 0xDDF2
+    hdr = bytes.fromhex("450000730000400040110000c0a80001c0a800c7")
+    assert (~dev.checksum(hdr, 0)) & 0xFFFF == 0xB861
+    for n in [0, 1, 2, 3, 7, 8, 15, 16, 17, 127, 128, 129, 1500, 65535]:
+        b = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        for ini in INITS:
+            assert dev.checksum(b, ini) == oracle.checksum(b, ini)
+    arena, pkts, kinds = synth.make_batch(8, 1500, kinds="mixed")
+    for i in range(8):
+        pkt = arena[pkts["off"][i]: pkts["off"][i] + 1500].tobytes()
+        v6 = bool(pkts["flags"][i] & PKT_V6)
+        proto = 17 if pkts["flags"][i] & PKT_UDP else 6
+        assert dev.checksum_valid(pkt, 40 if v6 else 20, proto, v6)
+        bad = bytearray(pkt)
+        bad[-1] ^= 1
+        assert not dev.checksum_valid(bytes(bad), 40 if v6 else 20, proto, v6)
+    rb = bytearray(rng.integers(0, 256, size=777, dtype=np.uint8).tobytes())
+    rb2 = bytearray(rb)
+    assert dev.gso_none_checksum(rb, 21, 16) is None
+    oracle.lib().or_gso_none_checksum((np.frombuffer(rb2, np.uint8)).ctypes.data, len(rb2), 21, 16)
+    assert rb == rb2

@@ -1,0 +1,212 @@
+// checksum_kernels.hip -- gfx950 (CDNA4) batch Internet-checksum kernels.
+//
+// Replaces, at batch granularity, the per-packet Go loops of
+//   checksum()                     /root/reference/tun/checksum.go:152-167
+//   checksumValid()                /root/reference/tun/gro.go:554-612
+//   gsoSplit's L4 checksum step    /root/reference/tun/gro.go:1469-1488
+//   gsoNoneChecksum()              /root/reference/tun/gro.go:1497-1517
+//   IPv4 header checksum sites     /root/reference/tun/gro.go:1134-1138,1434-1436
+//
+// Design: one wave64 per packet, persistent grid-stride
+// over packets.  Each lane streams 16-byte aligned chunks of the packet with
+// global_load_dwordx4 (1 KiB per wave instruction, U instructions in flight
+// per lane), masks head/tail/excluded bytes, and accumulates little-endian
+// u32 words into a u64.  Per-lane fold to 16 bits, DPP wave sum, parity
+// correction, pseudo-header / initial, final fold.  No LDS: each byte is read
+// once and used once (HBM-streaming reduction, cdna_hip_programming.md
+// "GEMV / M <= 16" row), no MFMA (byte reduction, not a contraction).
+#include <hip/hip_runtime.h>
+
+#include "../../include/wgcsum.h"
+#include "wgcs_common.h"
+#include "wgcs_kernels.h"
+
+namespace wgcs {
+
+// Per-packet byte-set description, all positions relative to the packet start.
+struct Ranges {
+  int main_lo, main_hi;  // summed range (BE word pairing starts at main_lo)
+  int addr_lo, addr_hi;  // pseudo-header address range (may be empty)
+  int fld;               // 2 excluded bytes at [fld, fld+2) (or far away)
+};
+
+// Masked contribution of one 16-byte chunk at packet position `pos`.
+__device__ __forceinline__ void add_chunk(uint64_t& acc, const uint4& v, int pos, const Ranges& r, bool rot_addr) {
+  const bool full = pos >= r.main_lo && pos + 16 <= r.main_hi && (pos >= r.addr_hi || pos + 16 <= r.addr_lo) &&
+                    (r.fld + 2 <= pos || r.fld >= pos + 16);
+  if (full) {
+    acc += (uint64_t)v.x + (uint64_t)v.y + (uint64_t)v.z + (uint64_t)v.w;
+  } else {
+    const int f = r.fld - pos;
+    uint32_t fb = 0;
+    if (f >= -1 && f < 16) fb = ((3u << (f + 1)) >> 1) & 0xFFFFu;
+    const uint32_t m16 = byte_bits16(r.main_lo - pos, r.main_hi - pos) & ~fb;
+    const uint32_t a16 = byte_bits16(r.addr_lo - pos, r.addr_hi - pos) & ~fb;  // the field is zeroed memory
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x = w[k] & expand_nibble((m16 >> (4 * k)) & 0xFu);
+      uint32_t y = w[k] & expand_nibble((a16 >> (4 * k)) & 0xFu);
+      if (rot_addr) y = rotl8(y);
+      acc += (uint64_t)x + (uint64_t)y;
+    }
+  }
+}
+
+// One packet per group of G lanes (G = 16: 4 packets per wave in flight; G = 64:
+// one wavefront per packet).  Each lane streams chunks c = sub + G*(u + U*it),
+// so one wave instruction reads 64/G contiguous 16*G-byte runs.
+template <int MODE, int G, int U, bool NT>
+__global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict__ arena,
+                                                             const wgcs_pkt* __restrict__ pkts,
+                                                             const uint64_t* __restrict__ initial,
+                                                             uint32_t n, void* __restrict__ out,
+                                                             int inplace) {
+  static_assert(G == 16 || G == 64, "group = DPP row or wave");
+  constexpr int PPW = 64 / G;  // packets per wave per step
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / G;
+  const int sub = lane % G;
+  const uint32_t wave =
+      (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+  const uint32_t step = gridDim.x * (blockDim.x >> 6) * PPW;
+  wgcs_pkt dn = {0, 0, 0, 0, 0};
+  {
+    const uint32_t p0 = wave * PPW + grp;
+    if (p0 < n) dn = pkts[p0];
+  }
+  for (uint32_t base = wave * PPW; base < n; base += step) {  // wave-uniform loop
+    const uint32_t p = base + grp;
+    const bool active = p < n;
+    const wgcs_pkt d = dn;
+    if (p + step < n) dn = pkts[p + step];  // prefetch the next descriptor
+    uint8_t* pkt = arena + d.off;
+    const int len = active ? (int)d.len : 0;
+    const int cs = d.csum_start;
+    const int co = d.csum_offset;
+    const bool v6 = (d.flags & WGCS_PKT_V6) != 0;
+    Ranges r;
+    r.main_lo = 0;
+    r.main_hi = len;
+    r.addr_lo = 0;
+    r.addr_hi = 0;
+    r.fld = -1000000;
+    uint32_t pre = 0;
+    uint64_t init = 0;
+    if (MODE == WGCS_MODE_FOLD) {
+      init = (initial && active) ? initial[p] : 0;
+    } else if (MODE == WGCS_MODE_L4_FILL || MODE == WGCS_MODE_VALIDATE) {
+      r.main_lo = min(cs, len);
+      r.addr_lo = min(v6 ? 8 : 12, len);
+      r.addr_hi = min(v6 ? 40 : 20, len);
+      if (MODE == WGCS_MODE_L4_FILL) r.fld = cs + co;
+      pre = ((d.flags & WGCS_PKT_UDP) ? 17u : 6u) + ((uint32_t)(len - cs) & 0xFFFFu);
+    } else if (MODE == WGCS_MODE_PARTIAL) {
+      r.main_lo = min(cs, len);
+      r.fld = (cs + co) & 0xFFFF;  // u16 arithmetic, gro.go:1503
+      if (r.fld + 1 < len) init = ((uint32_t)pkt[r.fld] << 8) | pkt[r.fld + 1];  // gro.go:1508
+    } else {  // WGCS_MODE_IP4HDR
+      r.main_hi = min(cs, len);
+      r.fld = 10;
+    }
+    const uintptr_t pbase = (uintptr_t)pkt;
+    const bool rot_addr = (((pbase + r.addr_lo) ^ (pbase + r.main_lo)) & 1u) != 0;
+    int lo_all = r.main_lo, hi_all = r.main_hi;
+    if (r.addr_hi > r.addr_lo) {
+      lo_all = min(lo_all, r.addr_lo);
+      hi_all = max(hi_all, r.addr_hi);
+    }
+    // keep pointer provenance from the kernel argument (global address space):
+    // an integer round trip would turn the loads into flat_load (full waits)
+    const int rel0 = lo_all - (int)((pbase + (uintptr_t)lo_all) & 15u);  // in [lo_all-15, lo_all]
+    const int nch = hi_all > lo_all ? (hi_all - rel0 + 15) >> 4 : 0;
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(pkt + rel0);
+    uint64_t acc = 0;
+    for (int c0 = sub; c0 < nch; c0 += G * U) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int c = c0 + u * G;
+        if (NT) {
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          u32x4 t = c < nch ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + c)) : u32x4{0, 0, 0, 0};
+          v[u] = make_uint4(t.x, t.y, t.z, t.w);
+        }
+        else v[u] = c < nch ? src[c] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) add_chunk(acc, v[u], rel0 + 16 * (c0 + u * G), r, rot_addr);
+    }
+    // all lanes converge here: per-lane fold, group sum, parity, pseudo/initial
+    uint32_t s = fold64_16(acc);
+    s = (G == 16) ? row16_sum_u32(s) : wave_sum_u32(s);
+    s = fold32_16(s);
+    if (((pbase + (uintptr_t)r.main_lo) & 1u) == 0) s = bswap16(s);
+    uint32_t t = fold32_16(s + pre + fold64_16(init));  // == the reference's checksum(...)
+    if (sub == 0 && active) {
+      if (MODE == WGCS_MODE_VALIDATE) {
+        reinterpret_cast<uint8_t*>(out)[p] = (t == 0xFFFFu) ? 1 : 0;  // ^checksum == 0
+      } else if (MODE == WGCS_MODE_FOLD) {
+        reinterpret_cast<uint16_t*>(out)[p] = (uint16_t)t;
+      } else {
+        const uint16_t c = (uint16_t)~t;
+        reinterpret_cast<uint16_t*>(out)[p] = c;
+        if (inplace && r.fld >= 0 && r.fld + 1 < len) {
+          pkt[r.fld] = (uint8_t)(c >> 8);
+          pkt[r.fld + 1] = (uint8_t)c;
+        }
+      }
+    }
+  }
+}
+
+template <int MODE>
+static hipError_t launch_mode(uint8_t* arena, const wgcs_pkt* pkts, const uint64_t* init, uint32_t n, void* out,
+                              int inplace, hipStream_t s, int num_cu, const LaunchTuning& t) {
+  const int ppb = (t.lanes_per_pkt == 64 ? 1 : 4) * 4;  // packets per block per step
+  long want = ((long)n + ppb - 1) / ppb;
+  long cap = (long)num_cu * t.blocks_per_cu;
+  const int grid = (int)(want < cap ? want : cap);
+#define WGCS_LAUNCH(G, U)                                                                                        \
+  do {                                                                                                            \
+    if (t.nt)                                                                                                     \
+      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, true>), dim3(grid), dim3(256), 0, s, arena, pkts, init, \
+                         n, out, inplace);                                                                        \
+    else                                                                                                          \
+      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, false>), dim3(grid), dim3(256), 0, s, arena, pkts,    \
+                         init, n, out, inplace);                                                                  \
+  } while (0)
+  if (t.lanes_per_pkt == 64) {
+    if (t.unroll >= 4) WGCS_LAUNCH(64, 4);
+    else WGCS_LAUNCH(64, 2);
+  } else {
+    if (t.unroll >= 8) WGCS_LAUNCH(16, 8);
+    else if (t.unroll >= 6) WGCS_LAUNCH(16, 6);
+    else WGCS_LAUNCH(16, 4);
+  }
+#undef WGCS_LAUNCH
+  return hipGetLastError();
+}
+
+hipError_t launch_checksum_batch(int mode, unsigned flags, uint8_t* arena, const wgcs_pkt* pkts,
+                                 const uint64_t* init, uint32_t n, void* out, hipStream_t s, int num_cu,
+                                 const LaunchTuning& tune) {
+  if (n == 0) return hipSuccess;
+  const int inplace = (flags & WGCS_F_INPLACE) ? 1 : 0;
+  switch (mode) {
+    case WGCS_MODE_FOLD:
+      return launch_mode<WGCS_MODE_FOLD>(arena, pkts, init, n, out, inplace, s, num_cu, tune);
+    case WGCS_MODE_L4_FILL:
+      return launch_mode<WGCS_MODE_L4_FILL>(arena, pkts, init, n, out, inplace, s, num_cu, tune);
+    case WGCS_MODE_VALIDATE:
+      return launch_mode<WGCS_MODE_VALIDATE>(arena, pkts, init, n, out, inplace, s, num_cu, tune);
+    case WGCS_MODE_PARTIAL:
+      return launch_mode<WGCS_MODE_PARTIAL>(arena, pkts, init, n, out, inplace, s, num_cu, tune);
+    case WGCS_MODE_IP4HDR:
+      return launch_mode<WGCS_MODE_IP4HDR>(arena, pkts, init, n, out, inplace, s, num_cu, tune);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace wgcs

@@ -1,0 +1,175 @@
+// gso_api.cpp -- C ABI for the GSO split path (include/wgcsum.h).
+//   wgcs_gso_split_batch     device-resident batch (one job per Tun.Read)
+//   wgcs_gso_split           gsoSplit()          /root/reference/tun/gro.go:1373-1493
+//   wgcs_handle_virtio_read  handleVirtioRead()  /root/reference/tun/tun.go:514-632
+// The host-buffer entry points stage the super-packet into HBM, run
+// gso_split_kernel (all validation, header rewriting, payload copies and
+// checksums happen there), and copy the produced segments back into the
+// caller's buffers.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+
+#include "../../include/wgcsum.h"
+#include "wgcs_ctx.h"
+#include "wgcs_kernels.h"
+
+using namespace wgcs;
+
+namespace {
+
+struct GsoResult {
+  int status = 0;
+  int count = 0;
+};
+
+// Runs one job through the kernel with bufs as the output slots.
+// vbuf = [10-byte virtio header | packet bytes] in host memory.
+int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflags, uint8_t* const* bufs,
+                 const size_t* buf_lens, int nbufs, int* sizes, int offset, GsoResult* res) {
+  if (nbufs <= 0 || !bufs || !buf_lens || !sizes || offset < 0)
+    return set_err(ctx, WGCS_ERR_INVALID_ARG, "bufs/sizes/offset");
+  if (vlen > 0x7FFFFFF0u) return set_err(ctx, WGCS_ERR_INVALID_ARG, "super-packet too large");
+  if (buf_lens[0] < (size_t)offset) return set_err(ctx, WGCS_ERR_OUT_OF_RANGE, "offset beyond bufs[0]");
+  // Device slots mirror bufs[0]'s capacity (the reference's room check for
+  // GSO_NONE is against bufs[0]); other buffers are checked after the kernel.
+  const size_t stride = std::min<size_t>(buf_lens[0], (size_t)offset + std::max<size_t>(vlen, 16));
+  std::lock_guard<std::mutex> g(ctx->mu);
+  hipSetDevice(ctx->device);
+  int rc;
+  const size_t meta = (size_t)nbufs * 4 + 16;
+  if ((rc = ensure_dev(ctx, ctx->d_arena, vlen + 32)) || (rc = ensure_dev(ctx, ctx->d_aux, sizeof(wgcs_gso_job))) ||
+      (rc = ensure_dev(ctx, ctx->d_out, (size_t)nbufs * stride + 16)) || (rc = ensure_dev(ctx, ctx->d_out2, meta)) ||
+      (rc = ensure_pinned(ctx, ctx->h_meta, meta + sizeof(wgcs_gso_job))))
+    return rc;
+  hipStream_t s = ctx->stream;
+  wgcs_gso_job* hjob = (wgcs_gso_job*)((uint8_t*)ctx->h_meta.ptr + meta);
+  hjob->off = 0;
+  hjob->len = (uint32_t)vlen;
+  hjob->flags = jflags;
+  int32_t* d_sizes = (int32_t*)ctx->d_out2.ptr;
+  int32_t* d_count = d_sizes + nbufs;
+  int32_t* d_status = d_count + 1;
+  hipError_t e = hipMemcpyAsync(ctx->d_arena.ptr, vbuf, vlen, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->d_aux.ptr, hjob, sizeof(wgcs_gso_job), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemsetAsync(d_sizes, 0, meta, s);
+  if (e != hipSuccess) return hip_fail(ctx, e, "H2D");
+  e = launch_gso_split_batch((const uint8_t*)ctx->d_arena.ptr, (const wgcs_gso_job*)ctx->d_aux.ptr, 1,
+                             (uint8_t*)ctx->d_out.ptr, (uint32_t)stride, (uint32_t)offset, (uint32_t)nbufs, d_sizes,
+                             d_count, d_status, s, ctx->num_cu);
+  if (e != hipSuccess) return hip_fail(ctx, e, "gso_split launch");
+  int32_t* h = (int32_t*)ctx->h_meta.ptr;
+  e = hipMemcpyAsync(h, d_sizes, meta, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(ctx, e, "D2H meta");
+  res->count = h[nbufs];
+  res->status = h[nbufs + 1];
+  if (res->status != 0 && res->status != WGCS_ERR_TOO_MANY_SEGMENTS) {
+    res->count = 0;
+    return WGCS_OK;
+  }
+  const int written = res->status == WGCS_ERR_TOO_MANY_SEGMENTS ? nbufs : res->count;
+  if (written <= 0) return WGCS_OK;
+  int maxsz = 0;
+  for (int i = 0; i < written; ++i) maxsz = std::max(maxsz, (int)h[i]);
+  const size_t width = (size_t)maxsz;
+  if ((rc = ensure_pinned(ctx, ctx->h_stage, (size_t)written * std::max<size_t>(width, 1)))) return rc;
+  e = hipMemcpy2DAsync(ctx->h_stage.ptr, std::max<size_t>(width, 1), (uint8_t*)ctx->d_out.ptr + offset, stride,
+                       width, (size_t)written, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(ctx, e, "D2H segments");
+  for (int i = 0; i < written; ++i) {
+    sizes[i] = h[i];
+    if (buf_lens[i] < (size_t)offset + (size_t)h[i]) {  // the Go code would panic on this slice
+      res->status = WGCS_ERR_OUT_OF_RANGE;
+      res->count = i;
+      return WGCS_OK;
+    }
+    memcpy(bufs[i] + offset, (uint8_t*)ctx->h_stage.ptr + (size_t)i * std::max<size_t>(width, 1), (size_t)h[i]);
+  }
+  return WGCS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wgcs_gso_split_batch(wgcs_ctx* ctx, const uint8_t* d_arena, const wgcs_gso_job* d_jobs, uint32_t n_jobs,
+                         uint8_t* d_out, uint32_t out_stride, uint32_t offset, uint32_t max_segs, int32_t* d_sizes,
+                         int32_t* d_count, int32_t* d_status, void* stream) {
+  if (!ctx) return WGCS_ERR_INVALID_ARG;
+  if (n_jobs == 0) return WGCS_OK;
+  if (!d_arena || !d_jobs || !d_out || !d_sizes || !d_count || !d_status || max_segs == 0)
+    return set_err(ctx, WGCS_ERR_INVALID_ARG, "NULL pointer or max_segs == 0");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  hipError_t e = launch_gso_split_batch(d_arena, d_jobs, n_jobs, d_out, out_stride, offset, max_segs, d_sizes, d_count,
+                                        d_status, s, ctx->num_cu);
+  return e == hipSuccess ? WGCS_OK : hip_fail(ctx, e, "gso_split_batch launch");
+}
+
+// gsoSplit(readBuf, hdr, bufs, sizes, offset, isV6) (int, error) -- gro.go:1373
+int wgcs_gso_split(wgcs_ctx* ctx, uint8_t* read_buf, size_t len, const wgcs_virtio_hdr* hdr, uint8_t* const* bufs,
+                   const size_t* buf_lens, int nbufs, int* sizes, int offset, int is_v6, int* n_out) {
+  if (!ctx || !hdr || !n_out || (!read_buf && len)) return WGCS_ERR_INVALID_ARG;
+  *n_out = 0;
+  int rc;
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if ((rc = ensure_pinned(ctx, ctx->h_out, len + 10))) return rc;
+  }
+  uint8_t* v = (uint8_t*)ctx->h_out.ptr;
+  v[0] = hdr->flags;
+  v[1] = hdr->gso_type;
+  memcpy(v + 2, &hdr->hdr_len, 2);
+  memcpy(v + 4, &hdr->gso_size, 2);
+  memcpy(v + 6, &hdr->csum_start, 2);
+  memcpy(v + 8, &hdr->csum_offset, 2);
+  if (len) memcpy(v + 10, read_buf, len);
+  GsoResult r;
+  rc = run_gso_host(ctx, v, len + 10, WGCS_GSO_JOB_RAW | (is_v6 ? WGCS_GSO_JOB_V6 : 0u), bufs, buf_lens, nbufs, sizes,
+                    offset, &r);
+  if (rc) return rc;
+  if (r.status == 0 || r.status == WGCS_ERR_TOO_MANY_SEGMENTS) {
+    // the reference zeroes these fields of readBuf before splitting (gro.go:1388,:1393)
+    if (!is_v6) read_buf[10] = read_buf[11] = 0;
+    const size_t at = (uint16_t)(hdr->csum_start + hdr->csum_offset);
+    read_buf[at] = read_buf[at + 1] = 0;
+  }
+  *n_out = r.count;
+  return r.status;
+}
+
+// handleVirtioRead(readBuf, bufs, sizes, offset) (int, error) -- tun/tun.go:514
+int wgcs_handle_virtio_read(wgcs_ctx* ctx, uint8_t* read_buf, size_t n, uint8_t* const* bufs, const size_t* buf_lens,
+                            int nbufs, int* sizes, int offset, int* n_out) {
+  if (!ctx || !n_out || (!read_buf && n)) return WGCS_ERR_INVALID_ARG;
+  *n_out = 0;
+  GsoResult r;
+  int rc = run_gso_host(ctx, read_buf, n, 0, bufs, buf_lens, nbufs, sizes, offset, &r);
+  if (rc) return rc;
+  if (n >= 10 && (r.status == 0 || r.status == WGCS_ERR_TOO_MANY_SEGMENTS)) {
+    uint8_t* rb = read_buf + 10;
+    uint16_t cs, co;
+    memcpy(&cs, read_buf + 6, 2);
+    memcpy(&co, read_buf + 8, 2);
+    const size_t at = (uint16_t)(cs + co);
+    if (read_buf[1] == 0) {
+      // GSO_NONE: gsoNoneChecksum wrote the checksum into readBuf (gro.go:1512-1515)
+      if (read_buf[0] & 1) {
+        rb[at] = bufs[0][offset + at];
+        rb[at + 1] = bufs[0][offset + at + 1];
+      }
+    } else {
+      if ((rb[0] >> 4) == 4) rb[10] = rb[11] = 0;  // gro.go:1388
+      rb[at] = rb[at + 1] = 0;                     // gro.go:1393
+    }
+  }
+  *n_out = r.count;
+  return r.status;
+}
+
+}  // extern "C"

@@ -1,0 +1,41 @@
+// wgcs_ctx.h -- the opaque wgcs_ctx of include/wgcsum.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <string>
+
+#include "../../include/wgcsum.h"
+#include "wgcs_kernels.h"
+
+namespace wgcs {
+
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t cap = 0;
+};
+struct HostBuf {
+  void* ptr = nullptr;
+  size_t cap = 0;
+};
+
+int set_err(wgcs_ctx* ctx, int code, const char* fmt, ...);
+int hip_fail(wgcs_ctx* ctx, hipError_t e, const char* what);
+int ensure_dev(wgcs_ctx* ctx, DevBuf& b, size_t bytes);
+int ensure_pinned(wgcs_ctx* ctx, HostBuf& b, size_t bytes);
+
+}  // namespace wgcs
+
+struct wgcs_ctx {
+  int device = 0;
+  int num_cu = 256;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string last_error;
+  wgcs::LaunchTuning tune;
+  // device staging (grown on demand, never shrunk)
+  wgcs::DevBuf d_arena, d_pkts, d_init, d_out, d_out2, d_aux;
+  // pinned host staging
+  wgcs::HostBuf h_stage, h_meta, h_out;
+};

@@ -1,0 +1,132 @@
+"""BASELINE.json configs[3] measurement: GSO split of 256 × 64-KiB TCP/IPv4
+super-segments into 1500-B MSS segments with per-segment checksums, on one
+MI355X (device-resident).  Called by bench.py --config cfg4.
+
+Per super-packet: 65,535 bytes read (the virtio header's 10 bytes included),
+45 segments written (44 × 1500 B + 1 × 1335 B; hdrLen 40, gsoSize 1460).
+Algorithmic bytes per launch = bytes read + bytes written.
+"""
+from __future__ import annotations
+
+import json
+import time
+
+import numpy as np
+
+from . import synth
+from .tun import GSO_JOB_DTYPE
+
+HBM_PEAK_GBS = 8000.0
+
+
+def run(args, torch, dev, dist, rank, world, local, barrier):
+    n_jobs, total, gso = 256, 65535, 1460
+    max_segs, stride, offset = 64, 1536, 16
+    R = max(args.rotate, 8)  # (16.8 MB in + 25 MB out) per copy: rotate past the 256 MiB MALL
+    pkts = [synth.make_super_packet(total, gso, seed=synth.SEED + 1000 * rank + k) for k in range(n_jobs)]
+    jlen = len(pkts[0])
+    arena = np.frombuffer(b"".join(pkts), dtype=np.uint8).copy()
+    jobs = np.zeros(n_jobs, GSO_JOB_DTYPE)
+    jobs["off"] = np.arange(n_jobs, dtype=np.uint64) * np.uint64(jlen)
+    jobs["len"] = jlen
+    stream = torch.cuda.Stream()
+    d_arena = [torch.from_numpy(arena).cuda() for _ in range(R)]
+    d_jobs = torch.from_numpy(jobs.view(np.uint8)).cuda()
+    d_out = [torch.empty(n_jobs * max_segs * stride, dtype=torch.uint8, device="cuda") for _ in range(R)]
+    d_sizes = torch.zeros(n_jobs * max_segs, dtype=torch.int32, device="cuda")
+    d_count = torch.zeros(n_jobs, dtype=torch.int32, device="cuda")
+    d_status = torch.zeros(n_jobs, dtype=torch.int32, device="cuda")
+
+    def step(k):
+        i = k % R
+        dev.gso_split_batch(d_arena[i], d_jobs, n_jobs, d_out[i], stride, offset, max_segs, d_sizes, d_count,
+                            d_status, stream=stream)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    count = d_count.cpu().numpy()
+    status = d_status.cpu().numpy()
+    assert (status == 0).all() and (count == 45).all(), (status[:4], count[:4])
+    sizes = d_sizes.cpu().numpy().reshape(n_jobs, max_segs)
+    bytes_out = int(sizes.astype(np.int64).sum())
+    bytes_in = int(jobs["len"].astype(np.int64).sum())
+    bytes_per_step = bytes_in + bytes_out
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for k in range(args.steps):
+        step(args.warmup + k)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = e0.elapsed_time(e1) / args.steps
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
+    result = {
+        "metric": "device-resident GSO split GiB/s (bytes read + written), 256×64KiB TCP/IPv4 → 1500-B MSS",
+        "value": round(bytes_per_step * args.steps * world / elapsed / 2**30, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {
+            "workload": "256 x 65535-B TCP/IPv4 super-packets -> 45 x <=1500-B segments each (gsoSize 1460), "
+                        "BASELINE.json configs[3]",
+            "segments_per_step": int((count).sum()),
+            "bytes_in": bytes_in,
+            "bytes_out": bytes_out,
+            "rotated_copies": R,
+            "parallelism": f"shard{world} (no collective)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel": "gso_split_kernel",
+            "kernel_ms": round(kern_ms, 5),
+            "algorithmic_bytes_per_launch": bytes_per_step,
+        },
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        result["cpu_baseline"] = cpu_baseline(pkts, args.cpu_seconds, bytes_per_step)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    dev.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(pkts, seconds, bytes_per_step):
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import oracle  # cpu_baseline leg only
+
+    bufs = [np.zeros(1536, np.uint8) for _ in range(64)]
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for p in pkts:
+            rb = np.frombuffer(bytearray(p), np.uint8)
+            oracle.handle_virtio_read(rb, bufs, 16)
+        reps += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(bytes_per_step * reps / dt / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} passes over the 256 super-packets, {dt:.1f} s, C restatement of handleVirtioRead+gsoSplit"}

@@ -1,0 +1,203 @@
+"""Host-side mirror of the reference's `tun` hot-path interface over the C ABI.
+
+Names, argument meaning and error behaviour follow /root/reference/tun:
+  checksum(b, initial)                     tun/checksum.go:152-167
+  checksum_valid(pkt, iph_len, proto, v6)  tun/gro.go:554-612
+  gso_none_checksum(read_buf, start, off)  tun/gro.go:1497-1517
+  gso_split(read_buf, hdr, bufs, sizes, offset, is_v6)      tun/gro.go:1373-1493
+  handle_virtio_read(read_buf, bufs, sizes, offset)         tun/tun.go:514-632
+  handle_gro(bufs, lens, offset, can_udp_gro)               tun/gro.go:1326-1367
+Go's `(n int, err error)` pairs become `(n, err)` tuples where `err` is None
+or a WgcsError carrying the status code (ErrTooManySegments keeps its n).
+
+Batch entry points (`checksum_batch`, `gso_split_batch`) take device
+pointers (ints) or torch tensors; torch is only used as the HBM allocator.
+Every byte is processed by the gfx950 kernels in libwgcsum.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import (MODE_FOLD, MODE_L4_FILL, MODE_VALIDATE, MODE_PARTIAL, MODE_IP4HDR, F_INPLACE, PKT_V6, PKT_UDP,
+                   VirtioHdr, WgcsError)
+
+PKT_DTYPE = np.dtype(
+    [("off", "<u8"), ("len", "<u4"), ("csum_start", "<u2"), ("csum_offset", "u1"), ("flags", "u1")]
+)
+GSO_JOB_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("pad", "<u4")])
+
+VIRTIO_NET_HDR_LEN = 10
+VIRTIO_NET_HDR_F_NEEDS_CSUM = 1
+VIRTIO_NET_HDR_GSO_NONE = 0
+VIRTIO_NET_HDR_GSO_TCPV4 = 1
+VIRTIO_NET_HDR_GSO_TCPV6 = 4
+VIRTIO_NET_HDR_GSO_UDP_L4 = 5
+
+__all__ = [
+    "Device", "PKT_DTYPE", "GSO_JOB_DTYPE", "MODE_FOLD", "MODE_L4_FILL", "MODE_VALIDATE", "MODE_PARTIAL",
+    "MODE_IP4HDR", "F_INPLACE", "PKT_V6", "PKT_UDP", "VirtioHdr", "WgcsError",
+]
+
+
+def _ptr(x) -> int | None:
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):  # torch tensor
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError(f"cannot take a pointer of {type(x)}")
+
+
+def _np_u8(buf) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        assert buf.dtype == np.uint8
+        return buf
+    return np.frombuffer(buf, dtype=np.uint8)
+
+
+class Device:
+    """One HIP context (stream + staging) on one GPU; `device` is the HIP ordinal."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        h = C.c_void_p()
+        rc = self.lib.wgcs_init(device, C.byref(h))
+        if rc != 0:
+            raise WgcsError(rc, self.lib.wgcs_strerror(rc).decode())
+        self.h = h
+        self.device = device
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.wgcs_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ utils
+    def _check(self, rc: int) -> None:
+        if rc != 0:
+            raise WgcsError(rc, self.lib.wgcs_last_error(self.h).decode() or self.lib.wgcs_strerror(rc).decode())
+
+    def _err(self, rc: int):
+        if rc == 0:
+            return None
+        if rc <= -100:  # HIP / allocation failures are exceptions, never values
+            self._check(rc)
+        return WgcsError(rc, self.lib.wgcs_last_error(self.h).decode() or self.lib.wgcs_strerror(rc).decode())
+
+    @property
+    def num_cu(self) -> int:
+        return self.lib.wgcs_num_cu(self.h)
+
+    def sync(self) -> None:
+        self._check(self.lib.wgcs_sync(self.h))
+
+    # ---------------------------------------------------------- device batch
+    def checksum_batch(self, mode: int, arena, pkts, n: int, out, initial=None, inplace: bool = False,
+                       stream=None) -> None:
+        """Asynchronous device-resident batch (HBM in, HBM out) on `stream`
+        (an int hipStream_t, a torch stream, or None for the context stream)."""
+        s = getattr(stream, "cuda_stream", stream)
+        self._check(self.lib.wgcs_checksum_batch(self.h, mode, F_INPLACE if inplace else 0, _ptr(arena), _ptr(pkts),
+                                                 _ptr(initial), n, _ptr(out), s))
+
+    def gso_split_batch(self, arena, jobs, n_jobs: int, out, out_stride: int, offset: int, max_segs: int, sizes,
+                        count, status, stream=None) -> None:
+        s = getattr(stream, "cuda_stream", stream)
+        self._check(self.lib.wgcs_gso_split_batch(self.h, _ptr(arena), _ptr(jobs), n_jobs, _ptr(out), out_stride,
+                                                  offset, max_segs, _ptr(sizes), _ptr(count), _ptr(status), s))
+
+    # ------------------------------------------------------------ host batch
+    def checksum_batch_host(self, mode: int, arena: np.ndarray, pkts: np.ndarray, initial=None,
+                            inplace: bool = False) -> np.ndarray:
+        assert pkts.dtype == PKT_DTYPE
+        n = len(pkts)
+        out = np.zeros(n, dtype=np.uint8 if mode == MODE_VALIDATE else np.uint16)
+        ini = None
+        if initial is not None:
+            ini = np.ascontiguousarray(initial, dtype=np.uint64)
+        self._check(self.lib.wgcs_checksum_batch_host(self.h, mode, F_INPLACE if inplace else 0, _ptr(arena),
+                                                      arena.nbytes, _ptr(pkts), _ptr(ini), n, _ptr(out)))
+        return out
+
+    # -------------------------------------------------- reference-shaped API
+    def checksum(self, b, initial: int = 0) -> int:
+        """checksum(b []byte, initial uint64) uint16 -- tun/checksum.go:152."""
+        a = _np_u8(bytes(b) if not isinstance(b, np.ndarray) else b)
+        out = C.c_uint16(0)
+        self._check(self.lib.wgcs_checksum(self.h, _ptr(a) if len(a) else None, len(a), initial & (2**64 - 1),
+                                           C.byref(out)))
+        return out.value
+
+    def checksum_valid(self, pkt, iph_len: int, proto: int, is_v6: bool) -> bool:
+        """checksumValid(pkt, iphLen, proto, isV6) -- tun/gro.go:554."""
+        a = _np_u8(bytes(pkt) if not isinstance(pkt, np.ndarray) else pkt)
+        v = C.c_int(0)
+        self._check(self.lib.wgcs_checksum_valid(self.h, _ptr(a), len(a), iph_len, proto, int(is_v6), C.byref(v)))
+        return bool(v.value)
+
+    def gso_none_checksum(self, read_buf, csum_start: int, csum_offset: int):
+        """gsoNoneChecksum(readBuf, csumStart, csumOffset) error -- mutates read_buf."""
+        a = _np_u8(read_buf)
+        return self._err(self.lib.wgcs_gso_none_checksum(self.h, _ptr(a), len(a), csum_start, csum_offset))
+
+    @staticmethod
+    def _bufs(bufs):
+        u8p = C.POINTER(C.c_uint8)
+        arr = (u8p * len(bufs))()
+        for i, b in enumerate(bufs):
+            arr[i] = C.cast(b.ctypes.data, u8p)
+        lens = (C.c_size_t * len(bufs))(*[len(b) for b in bufs])
+        return arr, lens
+
+    def gso_split(self, read_buf, hdr: VirtioHdr, bufs: list, sizes: list, offset: int, is_v6: bool):
+        """gsoSplit(readBuf, hdr, bufs, sizes, offset, isV6) (int, error)."""
+        a = _np_u8(read_buf)
+        arr, lens = self._bufs(bufs)
+        csz = (C.c_int * len(bufs))()
+        n = C.c_int(0)
+        rc = self.lib.wgcs_gso_split(self.h, _ptr(a), len(a), C.byref(hdr), arr, lens, len(bufs), csz, offset,
+                                     int(is_v6), C.byref(n))
+        sizes[: len(bufs)] = list(csz)
+        return n.value, self._err(rc)
+
+    def handle_virtio_read(self, read_buf, bufs: list, sizes: list, offset: int):
+        """handleVirtioRead(readBuf, bufs, sizes, offset) (int, error) -- tun/tun.go:514."""
+        a = _np_u8(read_buf)
+        arr, lens = self._bufs(bufs)
+        csz = (C.c_int * len(bufs))()
+        n = C.c_int(0)
+        rc = self.lib.wgcs_handle_virtio_read(self.h, _ptr(a), len(a), arr, lens, len(bufs), csz, offset,
+                                              C.byref(n))
+        sizes[: len(bufs)] = list(csz)
+        return n.value, self._err(rc)
+
+    def handle_gro(self, bufs: list, lens: list, offset: int, can_udp_gro: bool):
+        """handleGRO over Go-slice style buffers: bufs[i] is a numpy array whose
+        length is cap(bufs[i]); lens[i] = len(bufs[i]).  Returns
+        (to_write, order, new_lens, err): order[i] = index of the original
+        buffer now at position i (prepend swaps, gro.go:696-697)."""
+        n = len(bufs)
+        u8p = C.POINTER(C.c_uint8)
+        arr = (u8p * n)()
+        for i, b in enumerate(bufs):
+            arr[i] = C.cast(b.ctypes.data, u8p)
+        orig = [C.cast(arr[i], C.c_void_p).value for i in range(n)]
+        clens = (C.c_size_t * n)(*lens)
+        ccaps = (C.c_size_t * n)(*[len(b) for b in bufs])
+        tw = (C.c_int * max(n, 1))()
+        ntw = C.c_int(0)
+        rc = self.lib.wgcs_handle_gro(self.h, arr, clens, ccaps, n, offset, int(can_udp_gro), tw, C.byref(ntw))
+        order = [orig.index(C.cast(arr[i], C.c_void_p).value) for i in range(n)]
+        return list(tw)[: ntw.value], order, list(clens), self._err(rc)
