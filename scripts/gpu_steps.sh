@@ -26,6 +26,7 @@ for s in "$@"; do
     tests-all) step tests 1100 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     sweep) step sweep 400 python scripts/sweep_checksum.py ;;
     sweep-cfg3) step sweep_cfg3 400 python scripts/sweep_checksum.py --config cfg3 ;;
+    probe) step probe 400 python scripts/probe_stream.py ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 400 python bench.py --steps 200 --warmup 20 ;;
     bench-noevt) step bench_noevt 300 python bench.py --steps 200 --warmup 20 --no-event-timing --cpu-seconds 0 ;;

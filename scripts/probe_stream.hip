@@ -1,0 +1,81 @@
+// Roofline probe (NOT product code): the fastest plain streaming read this
+// chip sustains -- each wave sums U x 1 KiB aligned contiguous blocks with
+// global_load_dwordx4 and writes one word.  Built on the GPU box by
+// scripts/probe_stream.py; gives the practical HBM-read ceiling that the
+// checksum kernel is compared against.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void probe(const uint4* __restrict__ src, size_t n16, uint32_t* __restrict__ out) {
+  const size_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const size_t nw = (size_t)gridDim.x * 4;
+  const int lane = threadIdx.x & 63;
+  uint32_t acc = 0;
+  for (size_t b = wave * 64 * U; b < n16; b += nw * 64 * U) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      size_t c = b + u * 64 + lane;
+      if (NT) {
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        u4 t = c < n16 ? __builtin_nontemporal_load((const u4*)(src + c)) : u4{0, 0, 0, 0};
+        v[u] = make_uint4(t.x, t.y, t.z, t.w);
+      } else {
+        v[u] = c < n16 ? src[c] : make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+// Access pattern of checksum_batch_kernel<G=16,U>, minus all per-packet work:
+// each wave takes 4 consecutive packets of `stride` bytes, each 16-lane row
+// reads its packet's 16-B aligned chunks c = sub + 16u.
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void probe_rows(const uint8_t* __restrict__ arena, uint32_t npk, uint32_t stride,
+                                                  uint32_t* __restrict__ out) {
+  const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t nw = gridDim.x * 4;
+  const int lane = threadIdx.x & 63, grp = lane >> 4, sub = lane & 15;
+  uint32_t acc = 0;
+  for (uint32_t base = wave * 4; base < npk; base += nw * 4) {
+    const uint32_t p = base + grp;
+    const uint8_t* pkt = arena + (size_t)p * stride;
+    const int rel0 = 12 - (int)(((uintptr_t)pkt + 12) & 15);
+    const int nch = p < npk ? ((int)stride - rel0 + 15) >> 4 : 0;
+    const uint4* src = (const uint4*)(pkt + rel0);
+    for (int c0 = sub; c0 < nch; c0 += 16 * U) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        int c = c0 + 16 * u;
+        if (NT) {
+          typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+          u4 t = c < nch ? __builtin_nontemporal_load((const u4*)(src + c)) : u4{0, 0, 0, 0};
+          v[u] = make_uint4(t.x, t.y, t.z, t.w);
+        } else {
+          v[u] = c < nch ? src[c] : make_uint4(0, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+extern "C" int probe_rows_launch(const void* src, uint32_t npk, uint32_t stride, void* out, int grid, int nt,
+                                 void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (nt) hipLaunchKernelGGL((probe_rows<6, true>), dim3(grid), dim3(256), 0, s, (const uint8_t*)src, npk, stride, (uint32_t*)out);
+  else hipLaunchKernelGGL((probe_rows<6, false>), dim3(grid), dim3(256), 0, s, (const uint8_t*)src, npk, stride, (uint32_t*)out);
+  return (int)hipGetLastError();
+}
+extern "C" int probe_launch(const void* src, size_t bytes, void* out, int grid, int u, int nt, void* stream) {
+  size_t n16 = bytes / 16;
+  hipStream_t s = (hipStream_t)stream;
+#define L(U, NT) hipLaunchKernelGGL((probe<U, NT>), dim3(grid), dim3(256), 0, s, (const uint4*)src, n16, (uint32_t*)out)
+  if (nt) { if (u == 2) L(2, true); else if (u == 4) L(4, true); else L(8, true); }
+  else { if (u == 2) L(2, false); else if (u == 4) L(4, false); else L(8, false); }
+  return (int)hipGetLastError();
+}

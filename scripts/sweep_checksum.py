@@ -5,7 +5,7 @@ import argparse, os, sys, json
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-import torch
+import torch  # first: one HIP runtime per process
 from wireguard_amd import synth
 from wireguard_amd.tun import Device, MODE_VALIDATE, MODE_L4_FILL
 
@@ -13,7 +13,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="cfg2")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=100)
-ap.add_argument("--variants", default="16:4:8,16:6:8,16:8:8,64:2:8,64:4:8,16:6:4,16:4:4")
+ap.add_argument("--variants", default="16:6:4:0,16:6:4:1,16:6:8:1,16:4:8:1,16:8:8:1,64:4:8:1")
 ap.add_argument("--mode", default="validate")
 a = ap.parse_args()
 n, flen, kinds = {"cfg2": (65536, 1500, "tcp4"), "cfg3": (65536, 9000, "tcp4"), "cfg5": (131072, 1500, "mixed")}[a.config]
@@ -27,8 +27,9 @@ nbytes = int(pkts_np["len"].astype(np.int64).sum())
 stream = torch.cuda.Stream()
 devs = {}
 for v in a.variants.split(","):
-    g, u, b = v.split(":")
+    g, u, b, nt = v.split(":")
     os.environ["WGCS_LANES_PER_PKT"], os.environ["WGCS_UNROLL"], os.environ["WGCS_BLOCKS_PER_CU"] = g, u, b
+    os.environ["WGCS_NT"] = nt
     devs[v] = Device(0)
 res = {v: [] for v in devs}
 for r in range(a.rounds):
@@ -47,6 +48,6 @@ for r in range(a.rounds):
             assert bool(out[:n].all().item()), v
 for v, t in res.items():
     t = np.array(t)
-    print(json.dumps({"variant(G:U:BPC)": v, "config": a.config, "median_us": round(float(np.median(t)), 2),
+    print(json.dumps({"variant(G:U:BPC:NT)": v, "config": a.config, "median_us": round(float(np.median(t)), 2),
                       "min_us": round(float(t.min()), 2), "GBps": round(nbytes / np.median(t) / 1e3, 1),
                       "frac_8TBs": round(nbytes / np.median(t) / 1e3 / 8000, 3)}))

@@ -1,0 +1,103 @@
+"""CPU tests of the C ABI boundary (no GPU compute): the in-tree library
+loads, exports exactly the symbols include/wgcsum.h declares, the header is
+valid C with the documented struct layouts, and the Python mirror agrees with
+the header's constants.  Without a device, every compute entry fails loudly
+(there is no CPU fallback)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import wireguard_amd
+from wireguard_amd import _lib, tun
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "wgcsum.h")
+
+
+def _defines():
+    out = {}
+    for m in re.finditer(r"#define\s+(WGCS_\w+)\s+\(?(-?(?:0x)?[0-9a-fA-F]+)u?\)?", open(HDR).read()):
+        out[m.group(1)] = int(m.group(2), 0)
+    return out
+
+
+def test_library_exports_every_declared_symbol():
+    L = wireguard_amd.load()
+    declared = _lib.declared_symbols()
+    assert len(declared) >= 17
+    for name in declared:
+        assert hasattr(L, name), name
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = sorted({l.split()[-1] for l in nm.stdout.splitlines() if l.split()[-1].startswith("wgcs_")})
+    assert exported == declared
+    other = [l for l in nm.stdout.splitlines() if " T " in l and "wgcs_" not in l]
+    assert not other, f"unexpected exports: {other[:5]}"
+
+
+def test_header_is_c_and_layouts(tmp_path):
+    src = tmp_path / "t.c"
+    src.write_text(
+        '#include "wgcsum.h"\n#include <stddef.h>\n'
+        "_Static_assert(sizeof(wgcs_pkt) == 16, \"pkt\");\n"
+        "_Static_assert(offsetof(wgcs_pkt, len) == 8, \"len\");\n"
+        "_Static_assert(offsetof(wgcs_pkt, csum_start) == 12, \"cs\");\n"
+        "_Static_assert(offsetof(wgcs_pkt, flags) == 15, \"flags\");\n"
+        "_Static_assert(sizeof(wgcs_gso_job) == 16, \"job\");\n"
+        "_Static_assert(sizeof(wgcs_virtio_hdr) == 10, \"virtio_net_hdr is 10 bytes (gro.go:69-71)\");\n"
+        "int main(void) { return 0; }\n")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.dirname(HDR), str(src), "-o",
+                    str(tmp_path / "t")], check=True)
+
+
+def test_python_constants_match_header():
+    d = _defines()
+    for name, val in d.items():
+        short = name[len("WGCS_"):]
+        if hasattr(_lib, short):
+            assert getattr(_lib, short) == val, name
+    assert tun.PKT_DTYPE.itemsize == 16 and tun.GSO_JOB_DTYPE.itemsize == 16
+    assert C.sizeof(_lib.VirtioHdr) == 10
+    assert d["WGCS_MODE_VALIDATE"] == _lib.MODE_VALIDATE
+
+
+def test_version_and_errors():
+    L = wireguard_amd.load()
+    assert L.wgcs_abi_version() == _defines()["WGCS_ABI_VERSION"]
+    for code in [0, -1, -2, -3, -4, -5, -6, -7, -8, -9, -10, -11, -12, -13, -100, -101, -102]:
+        assert L.wgcs_strerror(code) and L.wgcs_strerror(code) != b"unknown status"
+    assert L.wgcs_strerror(-9999) == b"unknown status"
+
+
+def test_no_device_fails_loudly():
+    """In this container there is no GPU: the product must refuse, not fall back."""
+    L = wireguard_amd.load()
+    n = C.c_int(-1)
+    rc = L.wgcs_device_count(C.byref(n))
+    if rc == 0 and n.value > 0:
+        pytest.skip("a device is present")
+    with pytest.raises(_lib.WgcsError) as ei:
+        tun.Device(0)
+    assert ei.value.code == _lib.ERR_NO_DEVICE
+    # NULL-context calls are rejected without touching any device
+    assert L.wgcs_checksum_batch(None, 0, 0, None, None, None, 1, None, None) == _lib.ERR_INVALID_ARG
+    assert L.wgcs_gso_split_batch(None, None, None, 1, None, 0, 0, 1, None, None, None, None) == _lib.ERR_INVALID_ARG
+    assert L.wgcs_destroy(None) == _lib.ERR_INVALID_ARG
+
+
+def test_missing_library_raises(monkeypatch, tmp_path):
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(ImportError):
+        _lib.load()
+
+
+def test_synth_descriptors_layout():
+    from wireguard_amd import synth
+    arena, pkts, k = synth.make_batch(64, 1500, kinds="mixed")
+    assert pkts.dtype == tun.PKT_DTYPE
+    assert (pkts["off"] == np.arange(64) * 1500).all()
+    assert set(np.unique(pkts["csum_offset"])) <= {6, 16}

@@ -62,6 +62,9 @@ def declared_symbols() -> list[str]:
 
 
 def load() -> C.CDLL:
+    """Load libwgcsum.so.  If the process also uses torch, import torch FIRST:
+    torch ships its own libamdhip64.so.7 and the dynamic linker then binds our
+    library to that already-loaded runtime (one HIP runtime per process)."""
     global _lib
     if _lib is not None:
         return _lib

@@ -30,32 +30,42 @@ struct Ranges {
   int fld;               // 2 excluded bytes at [fld, fld+2) (or far away)
 };
 
-// Masked contribution of one 16-byte chunk at packet position `pos`.
-__device__ __forceinline__ void add_chunk(uint64_t& acc, const uint4& v, int pos, const Ranges& r, bool rot_addr) {
-  const bool full = pos >= r.main_lo && pos + 16 <= r.main_hi && (pos >= r.addr_hi || pos + 16 <= r.addr_lo) &&
-                    (r.fld + 2 <= pos || r.fld >= pos + 16);
-  if (full) {
-    acc += (uint64_t)v.x + (uint64_t)v.y + (uint64_t)v.z + (uint64_t)v.w;
-  } else {
-    const int f = r.fld - pos;
-    uint32_t fb = 0;
-    if (f >= -1 && f < 16) fb = ((3u << (f + 1)) >> 1) & 0xFFFFu;
-    const uint32_t m16 = byte_bits16(r.main_lo - pos, r.main_hi - pos) & ~fb;
-    const uint32_t a16 = byte_bits16(r.addr_lo - pos, r.addr_hi - pos) & ~fb;  // the field is zeroed memory
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+// Masked contribution of an edge chunk (head: addresses / gap / field; tail)
+// at packet position `pos`.
+__device__ __forceinline__ uint32_t edge_chunk(uint32_t acc, const uint4& v, int pos, const Ranges& r, bool rot_addr) {
+  const int f = r.fld - pos;
+  uint32_t fb = 0;
+  if (f >= -1 && f < 16) fb = ((3u << (f + 1)) >> 1) & 0xFFFFu;
+  const uint32_t m16 = byte_bits16(r.main_lo - pos, r.main_hi - pos) & ~fb;
+  const uint32_t a16 = byte_bits16(r.addr_lo - pos, r.addr_hi - pos) & ~fb;  // the field is zeroed memory
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t x = w[k] & expand_nibble((m16 >> (4 * k)) & 0xFu);
-      uint32_t y = w[k] & expand_nibble((a16 >> (4 * k)) & 0xFu);
-      if (rot_addr) y = rotl8(y);
-      acc += (uint64_t)x + (uint64_t)y;
-    }
+  for (int k = 0; k < 4; ++k) {
+    acc = add_halves(acc, w[k] & expand_nibble((m16 >> (4 * k)) & 0xFu));
+    uint32_t y = w[k] & expand_nibble((a16 >> (4 * k)) & 0xFu);
+    if (rot_addr) y = rotl8(y);  // 256*y (mod 2^32-1): address pairing parity differs from the main range
+    acc = add_halves(acc, y);
   }
+  return acc;
+}
+
+template <bool NT>
+__device__ __forceinline__ uint4 ld_chunk(const uint4* p) {
+  if (NT) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(t.x, t.y, t.z, t.w);
+  }
+  return *p;
 }
 
 // One packet per group of G lanes (G = 16: 4 packets per wave in flight; G = 64:
-// one wavefront per packet).  Each lane streams chunks c = sub + G*(u + U*it),
-// so one wave instruction reads 64/G contiguous 16*G-byte runs.
+// one wavefront per packet).  The packet's 16-byte chunks are split into
+// "edge" chunks (the first ones, up to the end of the address range / gap /
+// checksum field, and a partial last one) that need byte masks, and interior
+// chunks that are summed unmasked: lanes stream interior chunk
+// c = c_lo + sub + G*(u + U*it), so one wave instruction reads 64/G
+// contiguous 16*G-byte runs, and each lane owns at most a few edge chunks.
 template <int MODE, int G, int U, bool NT>
 __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict__ arena,
                                                              const wgcs_pkt* __restrict__ pkts,
@@ -111,34 +121,54 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
     }
     const uintptr_t pbase = (uintptr_t)pkt;
     const bool rot_addr = (((pbase + r.addr_lo) ^ (pbase + r.main_lo)) & 1u) != 0;
-    int lo_all = r.main_lo, hi_all = r.main_hi;
+    int lo_all = r.main_lo, hi_all = r.main_hi, hole_end = r.main_lo;
     if (r.addr_hi > r.addr_lo) {
       lo_all = min(lo_all, r.addr_lo);
       hi_all = max(hi_all, r.addr_hi);
+      hole_end = max(hole_end, r.addr_hi);
     }
+    if (r.fld + 2 > lo_all && r.fld < hi_all) hole_end = max(hole_end, r.fld + 2);
     // keep pointer provenance from the kernel argument (global address space):
     // an integer round trip would turn the loads into flat_load (full waits)
     const int rel0 = lo_all - (int)((pbase + (uintptr_t)lo_all) & 15u);  // in [lo_all-15, lo_all]
     const int nch = hi_all > lo_all ? (hi_all - rel0 + 15) >> 4 : 0;
+    int c_lo = min((hole_end - rel0 + 15) >> 4, nch);  // first unmasked chunk
+    int c_hi = max((hi_all - rel0) >> 4, c_lo);        // end of unmasked chunks
+    const int n_edge = c_lo + (nch - c_hi);
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(pkt + rel0);
-    uint64_t acc = 0;
-    for (int c0 = sub; c0 < nch; c0 += G * U) {
+    uint32_t acc = 0;
+    // edge chunks: issued first, consumed after the first interior batch is in flight
+    int ce = sub < c_lo ? sub : c_hi + (sub - c_lo);
+    uint4 ve = sub < n_edge ? ld_chunk<NT>(src + ce) : make_uint4(0, 0, 0, 0);
+    bool edge_pending = true;
+    for (int c0 = c_lo + sub; c0 < c_hi || edge_pending; c0 += G * U) {
       uint4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int c = c0 + u * G;
-        if (NT) {
-          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-          u32x4 t = c < nch ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + c)) : u32x4{0, 0, 0, 0};
-          v[u] = make_uint4(t.x, t.y, t.z, t.w);
-        }
-        else v[u] = c < nch ? src[c] : make_uint4(0, 0, 0, 0);
+        v[u] = c < c_hi ? ld_chunk<NT>(src + c) : make_uint4(0, 0, 0, 0);
       }
+      if (edge_pending) {
+        for (int e = sub;;) {  // rows with more than G edge chunks (long field offsets) loop
+          if (e < n_edge) acc = edge_chunk(acc, ve, rel0 + 16 * ce, r, rot_addr);
+          e += G;
+          if (e >= n_edge) break;
+          ce = e < c_lo ? e : c_hi + (e - c_lo);
+          ve = ld_chunk<NT>(src + ce);
+        }
+        edge_pending = false;
+      }
+      acc = (acc >> 16) + (acc & 0xFFFFu);  // keep the u32 partial sum far from overflow (huge packets)
 #pragma unroll
-      for (int u = 0; u < U; ++u) add_chunk(acc, v[u], rel0 + 16 * (c0 + u * G), r, rot_addr);
+      for (int u = 0; u < U; ++u) {
+        acc = add_halves(acc, v[u].x);
+        acc = add_halves(acc, v[u].y);
+        acc = add_halves(acc, v[u].z);
+        acc = add_halves(acc, v[u].w);
+      }
     }
     // all lanes converge here: per-lane fold, group sum, parity, pseudo/initial
-    uint32_t s = fold64_16(acc);
+    uint32_t s = fold32_16(acc);
     s = (G == 16) ? row16_sum_u32(s) : wave_sum_u32(s);
     s = fold32_16(s);
     if (((pbase + (uintptr_t)r.main_lo) & 1u) == 0) s = bswap16(s);

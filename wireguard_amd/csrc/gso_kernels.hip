@@ -25,6 +25,7 @@
 
 #include "../../include/wgcsum.h"
 #include "wgcs_common.h"
+#include "wgcs_copy.h"
 #include "wgcs_kernels.h"
 
 namespace wgcs {
@@ -33,113 +34,39 @@ namespace {
 
 constexpr int kHdrLds = 256;   // LDS bytes per wave for the segment headers
 constexpr int kMaxHdrLen = 240;  // hdrLen + dest phase (<= 15) must fit kHdrLds
+constexpr int kSlotsPerWave = 2;  // output segments per wave (amortizes the header decode)
 
 enum : int { GSO_NONE = 0, GSO_TCPV4 = 1, GSO_TCPV6 = 4, GSO_UDP_L4 = 5 };
 
 __device__ __forceinline__ uint32_t u8at(const uint8_t* p) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)*p); }
-__device__ __forceinline__ uint32_t le16at(const uint8_t* p) { return u8at(p) | (u8at(p + 1) << 8); }
 __device__ __forceinline__ uint32_t be16at(const uint8_t* p) { return (u8at(p) << 8) | u8at(p + 1); }
-__device__ __forceinline__ uint32_t be32at(const uint8_t* p) { return (be16at(p) << 16) | be16at(p + 2); }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// All addresses stay pointers derived from kernel arguments (no integer round
-// trips), so the compiler keeps them in the global address space and emits
-// global_load/store (not flat_*, which forces full vmcnt+lgkmcnt waits).
-__device__ __forceinline__ uint4 ld16(const uint8_t* a) { return *reinterpret_cast<const uint4*>(a); }
-
-// Funnel: bytes [s, s+16) of the 32-byte concatenation a|b (s wave-uniform).
-__device__ __forceinline__ uint4 funnel(const uint4& a, const uint4& b, int s) {
-  const int r = s & 3;
-  uint32_t d0 = a.x, d1 = a.y, d2 = a.z, d3 = a.w, d4 = b.x, d5 = b.y, d6 = b.z, d7 = b.w;
-  uint32_t e0, e1, e2, e3, e4;
-  switch (s >> 2) {
-    case 0: e0 = d0; e1 = d1; e2 = d2; e3 = d3; e4 = d4; break;
-    case 1: e0 = d1; e1 = d2; e2 = d3; e3 = d4; e4 = d5; break;
-    case 2: e0 = d2; e1 = d3; e2 = d4; e3 = d5; e4 = d6; break;
-    default: e0 = d3; e1 = d4; e2 = d5; e3 = d6; e4 = d7; break;
+// The first 256 bytes of a job ([virtio hdr | packet...]) held across the
+// wave, one byte per lane per register: a single batch of byte loads instead
+// of a chain of dependent scalar reads.  byte(k) for uniform k < 256.
+struct HdrBytes {
+  uint32_t r0, r1, r2, r3;
+  int len;
+  const uint8_t* base;
+  __device__ __forceinline__ void load(const uint8_t* vb, int n, int lane) {
+    base = vb;
+    len = n;
+    r0 = lane < n ? vb[lane] : 0u;
+    r1 = lane + 64 < n ? vb[lane + 64] : 0u;
+    r2 = lane + 128 < n ? vb[lane + 128] : 0u;
+    r3 = lane + 192 < n ? vb[lane + 192] : 0u;
   }
-  uint4 o;
-  o.x = __builtin_amdgcn_alignbyte(e1, e0, r);
-  o.y = __builtin_amdgcn_alignbyte(e2, e1, r);
-  o.z = __builtin_amdgcn_alignbyte(e3, e2, r);
-  o.w = __builtin_amdgcn_alignbyte(e4, e3, r);
-  return o;
-}
-
-__device__ __forceinline__ uint32_t chunk_byte(const uint4& v, int j) {
-  const uint32_t w = j < 4 ? v.x : (j < 8 ? v.y : (j < 12 ? v.z : v.w));
-  return (w >> (8 * (j & 3))) & 0xFFu;
-}
-
-__device__ __forceinline__ uint4 set_chunk_byte(uint4 v, int j, uint32_t b) {
-  const uint32_t sh = 8 * (j & 3), m = ~(0xFFu << sh), x = (b & 0xFFu) << sh;
-  if (j < 4) v.x = (v.x & m) | x;
-  else if (j < 8) v.y = (v.y & m) | x;
-  else if (j < 12) v.z = (v.z & m) | x;
-  else v.w = (v.w & m) | x;
-  return v;
-}
-
-// Masked LE sum of the chunk's bytes at packet positions [lo, hi) (chunk at x0).
-__device__ __forceinline__ uint64_t chunk_sum(const uint4& v, int x0, int lo, int hi) {
-  if (x0 >= lo && x0 + 16 <= hi) return (uint64_t)v.x + v.y + v.z + v.w;
-  const uint32_t m16 = byte_bits16(lo - x0, hi - x0);
-  return (uint64_t)(v.x & expand_nibble(m16 & 0xF)) + (v.y & expand_nibble((m16 >> 4) & 0xF)) +
-         (v.z & expand_nibble((m16 >> 8) & 0xF)) + (v.w & expand_nibble((m16 >> 12) & 0xF));
-}
-
-// Store the part of a destination chunk that lies in [0, pkt_len).
-__device__ __forceinline__ void store_chunk(uint8_t* dchunk, const uint4& v, int x0, int pkt_len) {
-  if (x0 >= 0 && x0 + 16 <= pkt_len) {
-    *reinterpret_cast<uint4*>(dchunk) = v;
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int x = x0 + j;
-      if (x >= 0 && x < pkt_len) dchunk[j] = (uint8_t)chunk_byte(v, j);
-    }
+  __device__ __forceinline__ uint32_t operator()(int k) const {  // k wave-uniform
+    if (k >= 256) return u8at(base + k);
+    const int l = k & 63;
+    const uint32_t v = k < 64 ? r0 : (k < 128 ? r1 : (k < 192 ? r2 : r3));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
   }
-}
-
-// Copy source positions -> destination chunks [k_begin, k_end) of a packet
-// whose byte x lives at src0 + x (source bytes valid in [src_lo, src_hi)),
-// destination chunk k covering packet positions [16k - dalign, +16).  Sums the
-// bytes at positions [sum_lo, pkt_len) into acc; optionally overrides the two
-// bytes at [pf, pf+2) with the big-endian value pv.
-__device__ __forceinline__ void stream_copy(const uint8_t* src0, const uint8_t* src_lo, const uint8_t* src_hi,
-                                            uint8_t* dbase, int dalign, int k_begin, int k_end, int pkt_len,
-                                            int sum_lo, int pf, uint32_t pv, int lane, uint64_t& acc) {
-  const uint8_t* w0 = src0 - dalign;  // source address of dest chunk 0's first byte
-  const int s = (int)((uintptr_t)w0 & 15);
-  const uint8_t* abase = w0 - s;
-  for (int k0 = k_begin; k0 < k_end; k0 += 64) {
-    const int k = k0 + lane;
-    const uint8_t* ca = abase + 16 * (long)k;
-    uint4 a = make_uint4(0, 0, 0, 0);
-    if (ca < src_hi && ca + 16 > src_lo) a = ld16(ca);
-    uint4 b;
-    b.x = __shfl_down(a.x, 1);
-    b.y = __shfl_down(a.y, 1);
-    b.z = __shfl_down(a.z, 1);
-    b.w = __shfl_down(a.w, 1);
-    if (lane == 63) {
-      const uint8_t* cb = ca + 16;
-      b = make_uint4(0, 0, 0, 0);
-      if (cb < src_hi && cb + 16 > src_lo) b = ld16(cb);
-    }
-    if (k < k_end) {
-      uint4 v = funnel(a, b, s);
-      const int x0 = 16 * k - dalign;
-      if (pf >= 0) {
-        const int j0 = pf - x0, j1 = pf + 1 - x0;
-        if (j0 >= 0 && j0 < 16) v = set_chunk_byte(v, j0, pv >> 8);
-        if (j1 >= 0 && j1 < 16) v = set_chunk_byte(v, j1, pv);
-      }
-      acc += chunk_sum(v, x0, sum_lo, pkt_len);
-      store_chunk(dbase + 16 * k, v, x0, pkt_len);
-    }
-  }
-}
+  __device__ __forceinline__ uint32_t le16(int k) const { return (*this)(k) | ((*this)(k + 1) << 8); }
+  __device__ __forceinline__ uint32_t be16(int k) const { return ((*this)(k) << 8) | (*this)(k + 1); }
+  __device__ __forceinline__ uint32_t be32(int k) const { return (be16(k) << 16) | be16(k + 2); }
+};
 
 struct Job {
   int status;    // 0 or WGCS_ERR_*
@@ -182,16 +109,15 @@ __device__ bool split_bounds_ok(const Job& j) {
 }
 
 // handleVirtioRead's checks (tun/tun.go:522-630) + this kernel's limits.
-__device__ Job decode_job(const uint8_t* vb, uint32_t len, uint32_t jflags, uint32_t out_room, uint32_t max_segs) {
+__device__ Job decode_job(const HdrBytes& hb, uint32_t len, uint32_t jflags, uint32_t out_room, uint32_t max_segs) {
   Job j = {};
   if (len < 10) { j.status = WGCS_ERR_SHORT_BUFFER; return j; }  // gro.go:84-86
-  j.flags = (int)u8at(vb);
-  j.type = (int)u8at(vb + 1);
-  j.hdr_len = (int)le16at(vb + 2);
-  j.gso = (int)le16at(vb + 4);
-  j.cs = (int)le16at(vb + 6);
-  j.co = (int)le16at(vb + 8);
-  const uint8_t* rb = vb + 10;
+  j.flags = (int)hb(0);
+  j.type = (int)hb(1);
+  j.hdr_len = (int)hb.le16(2);
+  j.gso = (int)hb.le16(4);
+  j.cs = (int)hb.le16(6);
+  j.co = (int)hb.le16(8);
   const int plen = (int)len - 10;
   j.plen = plen;
   if (jflags & WGCS_GSO_JOB_RAW) {  // gsoSplit with the caller's header (gro.go:1373)
@@ -216,7 +142,7 @@ __device__ Job decode_job(const uint8_t* vb, uint32_t len, uint32_t jflags, uint
     return j;
   }
   if (plen < 1) { j.status = WGCS_ERR_OUT_OF_RANGE; return j; }
-  j.ipv = (int)(u8at(rb) >> 4);  // :570
+  j.ipv = (int)(hb(10) >> 4);  // :570
   if (j.ipv == 4) {
     if (j.type != GSO_TCPV4 && j.type != GSO_UDP_L4) { j.status = WGCS_ERR_IP_GSO_MISMATCH; return j; }
   } else if (j.ipv == 6) {
@@ -230,7 +156,7 @@ __device__ Job decode_job(const uint8_t* vb, uint32_t len, uint32_t jflags, uint
   } else {
     const int at = (j.cs + 12) & 0xFFFF;
     if (plen <= at) { j.status = WGCS_ERR_PACKET_TOO_SHORT; return j; }
-    const int th = (int)((u8at(rb + at) >> 4) * 4);
+    const int th = (int)((hb(10 + at) >> 4) * 4);
     if (th < 20 || th > 60) { j.status = WGCS_ERR_TCP_HDR_LEN; return j; }
     j.hdr_len = (j.cs + th) & 0xFFFF;
   }
@@ -275,10 +201,11 @@ __device__ void none_segment(const uint8_t* rb, const Job& j, uint8_t* dst, int 
   uint8_t* dbase = dst - dalign;
   const int nk = (plen + dalign + 15) >> 4;
   uint64_t dummy = 0;
-  stream_copy(rb, rb, rb + plen, dbase, dalign, 0, nk, plen, plen, pf, pv, lane, dummy);
+  stream_copy<false>(rb, rb, rb + plen, dbase, dalign, 0, nk, plen, plen, pf, pv, lane, dummy);
 }
 
-__device__ void gso_segment(const uint8_t* rb, const Job& j, int i, uint8_t* dst, uint8_t* lds, int lane) {
+__device__ void gso_segment(const uint8_t* rb, const HdrBytes& hb, const Job& j, int i, uint8_t* dst, uint8_t* lds,
+                            int lane) {
   const bool v4 = j.ipv == 4;
   const bool tcp = j.type != GSO_UDP_L4;
   const int hdr_len = j.hdr_len, cs = j.cs, plen = j.plen;
@@ -289,9 +216,9 @@ __device__ void gso_segment(const uint8_t* rb, const Job& j, int i, uint8_t* dst
   const int pkt_len = hdr_len + seg_len;
   const int csum_at = (cs + j.co) & 0xFFFF;
   // per-segment header values (gro.go:1419-1466)
-  const uint32_t id0 = v4 ? be16at(rb + 4) : 0;
+  const uint32_t id0 = v4 ? hb.be16(10 + 4) : 0;
   const uint32_t id1 = (id0 + 1) & 0xFFFF;                                     // quirk: +1 for every i >= 1
-  const uint32_t first_seq = tcp ? be32at(rb + cs + 4) : 0;
+  const uint32_t first_seq = tcp ? hb.be32(10 + cs + 4) : 0;
   const uint32_t seq = first_seq + (uint32_t)(uint16_t)((uint16_t)j.gso * (uint16_t)i);  // uint16 product
   const bool last = seg_end == plen;
   const uint32_t ulen = (uint32_t)(uint16_t)(seg_len + (hdr_len - cs));
@@ -362,7 +289,7 @@ __device__ void gso_segment(const uint8_t* rb, const Job& j, int i, uint8_t* dst
     hv = *reinterpret_cast<const uint4*>(lds + 16 * lane);
     acc += chunk_sum(hv, 16 * lane - dalign, cs, pkt_len);
   }
-  stream_copy(pay_src0, rb + seg_start, rb + seg_end, dbase, dalign, hk, nk, pkt_len, cs, -1, 0, lane, acc);
+  stream_copy<true>(pay_src0, rb + seg_start, rb + seg_end, dbase, dalign, hk, nk, pkt_len, cs, -1, 0, lane, acc);
   uint32_t s = fold32_16(wave_sum_u32(fold64_16(acc)));
   if ((((uintptr_t)dst + (uintptr_t)cs) & 1u) == 0) s = bswap16(s);
   const uint32_t proto = tcp ? 6u : 17u;
@@ -393,32 +320,38 @@ __global__ __launch_bounds__(256) void gso_split_kernel(const uint8_t* __restric
   uint8_t* lds = lds_all[wv];
   const uint64_t wave = (uint64_t)uni((int)(blockIdx.x * 4 + wv));
   const uint64_t nwaves = (uint64_t)gridDim.x * 4;
-  const uint64_t total = (uint64_t)n_jobs * max_segs;
   const uint32_t room = out_stride > offset ? out_stride - offset : 0;
-  for (uint64_t slot = wave; slot < total; slot += nwaves) {
-    const uint32_t jb = (uint32_t)(slot / max_segs);
-    const int i = (int)(slot - (uint64_t)jb * max_segs);
+  const uint32_t groups_per_job = (max_segs + kSlotsPerWave - 1) / kSlotsPerWave;
+  const uint64_t total_groups = (uint64_t)n_jobs * groups_per_job;
+  for (uint64_t g = wave; g < total_groups; g += nwaves) {
+    const uint32_t jb = (uint32_t)(g / groups_per_job);
+    const int i0 = (int)(g - (uint64_t)jb * groups_per_job) * kSlotsPerWave;
     const uint64_t joff = jobs[jb].off;
     const uint32_t jlen = jobs[jb].len;
     const uint32_t jflags = jobs[jb].flags;
     const uint8_t* vb = arena + joff;
-    const Job j = decode_job(vb, jlen, jflags, room, max_segs);
-    if (i == 0 && lane == 0) {
+    HdrBytes hb;
+    hb.load(vb, (int)min(jlen, 256u), lane);
+    const Job j = decode_job(hb, jlen, jflags, room, max_segs);
+    if (i0 == 0 && lane == 0) {
       count[jb] = j.status && j.status != WGCS_ERR_TOO_MANY_SEGMENTS ? 0 : j.count;
       status[jb] = j.status;
     }
     if (j.status && j.status != WGCS_ERR_TOO_MANY_SEGMENTS) continue;
-    if (i >= j.nseg) continue;
-    uint8_t* dst = out + slot * (uint64_t)out_stride + offset;
-    if (j.type == GSO_NONE) {
-      none_segment(vb + 10, j, dst, lane);
-      if (lane == 0) sizes[slot] = j.plen;
-    } else {
-      gso_segment(vb + 10, j, i, dst, lds, lane);
-      if (lane == 0) {
-        const long seg_start = (long)j.hdr_len + (long)i * j.gso;
-        const long seg_end = min((long)j.plen, seg_start + j.gso);
-        sizes[slot] = (int32_t)(j.hdr_len + (seg_end - seg_start));
+    const int i_end = min(i0 + kSlotsPerWave, j.nseg);
+    for (int i = i0; i < i_end; ++i) {
+      const uint64_t slot = (uint64_t)jb * max_segs + i;
+      uint8_t* dst = out + slot * (uint64_t)out_stride + offset;
+      if (j.type == GSO_NONE) {
+        none_segment(vb + 10, j, dst, lane);
+        if (lane == 0) sizes[slot] = j.plen;
+      } else {
+        gso_segment(vb + 10, hb, j, i, dst, lds, lane);
+        if (lane == 0) {
+          const long seg_start = (long)j.hdr_len + (long)i * j.gso;
+          const long seg_end = min((long)j.plen, seg_start + j.gso);
+          sizes[slot] = (int32_t)(j.hdr_len + (seg_end - seg_start));
+        }
       }
     }
   }
@@ -428,8 +361,8 @@ hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs
                                   uint32_t out_stride, uint32_t offset, uint32_t max_segs, int32_t* sizes,
                                   int32_t* count, int32_t* status, hipStream_t s, int num_cu) {
   if (n_jobs == 0 || max_segs == 0) return hipSuccess;
-  const uint64_t slots = (uint64_t)n_jobs * max_segs;
-  uint64_t want = (slots + 3) / 4;
+  const uint64_t groups = (uint64_t)n_jobs * ((max_segs + kSlotsPerWave - 1) / kSlotsPerWave);
+  uint64_t want = (groups + 3) / 4;
   const uint64_t cap = (uint64_t)num_cu * 8;
   const int grid = (int)(want < cap ? want : cap);
   hipLaunchKernelGGL(gso_split_kernel, dim3(grid), dim3(256), 0, s, arena, jobs, n_jobs, out, out_stride, offset,

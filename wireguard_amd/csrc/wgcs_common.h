@@ -73,6 +73,16 @@ __device__ __forceinline__ uint32_t byte_bits16(int lo, int hi) {
   return h & ~l;
 }
 
+// acc + lo16(w) + hi16(w) in ONE instruction (v_dot2_u32_u16 with {1,1}):
+// w ≡ lo16 + hi16 (mod 0xFFFF) and the sum is 0 iff w is 0, so a u32 of these
+// is an exact, zero-preserving partial sum as long as it cannot overflow
+// (< 2^15 dwords per accumulator).
+__device__ __forceinline__ uint32_t add_halves(uint32_t acc, uint32_t w) {
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  const us2 one = {1, 1};
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(us2, w), one, acc, false);
+}
+
 // Expand a 4-bit byte mask into a 32-bit byte mask (bit j -> byte j = 0xFF).
 __device__ __forceinline__ uint32_t expand_nibble(uint32_t nib) {
   return ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;

@@ -1,0 +1,148 @@
+// wgcs_copy.h -- device helpers for byte-stream copies between arbitrary
+// source / destination alignments (GSO split and GRO coalesce kernels).
+// Destination-aligned 16-byte chunks are assembled from aligned source loads
+// with a cross-lane neighbour fetch and a uniform funnel shift, so every HBM
+// load and every full-chunk store is a 16-byte global_load/store_dwordx4.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "wgcs_common.h"
+
+namespace wgcs {
+
+// All addresses stay pointers derived from kernel arguments (no integer round
+// trips), so the compiler keeps them in the global address space and emits
+// global_load/store (not flat_*, which forces full vmcnt+lgkmcnt waits).
+__device__ __forceinline__ uint4 ld16(const uint8_t* a) { return *reinterpret_cast<const uint4*>(a); }
+
+// Funnel: bytes [s, s+16) of the 32-byte concatenation a|b (s wave-uniform).
+__device__ __forceinline__ uint4 funnel(const uint4& a, const uint4& b, int s) {
+  const int r = s & 3;
+  uint32_t d0 = a.x, d1 = a.y, d2 = a.z, d3 = a.w, d4 = b.x, d5 = b.y, d6 = b.z, d7 = b.w;
+  uint32_t e0, e1, e2, e3, e4;
+  switch (s >> 2) {
+    case 0: e0 = d0; e1 = d1; e2 = d2; e3 = d3; e4 = d4; break;
+    case 1: e0 = d1; e1 = d2; e2 = d3; e3 = d4; e4 = d5; break;
+    case 2: e0 = d2; e1 = d3; e2 = d4; e3 = d5; e4 = d6; break;
+    default: e0 = d3; e1 = d4; e2 = d5; e3 = d6; e4 = d7; break;
+  }
+  uint4 o;
+  o.x = __builtin_amdgcn_alignbyte(e1, e0, r);
+  o.y = __builtin_amdgcn_alignbyte(e2, e1, r);
+  o.z = __builtin_amdgcn_alignbyte(e3, e2, r);
+  o.w = __builtin_amdgcn_alignbyte(e4, e3, r);
+  return o;
+}
+
+__device__ __forceinline__ uint32_t chunk_byte(const uint4& v, int j) {
+  const uint32_t w = j < 4 ? v.x : (j < 8 ? v.y : (j < 12 ? v.z : v.w));
+  return (w >> (8 * (j & 3))) & 0xFFu;
+}
+
+__device__ __forceinline__ uint4 set_chunk_byte(uint4 v, int j, uint32_t b) {
+  const uint32_t sh = 8 * (j & 3), m = ~(0xFFu << sh), x = (b & 0xFFu) << sh;
+  if (j < 4) v.x = (v.x & m) | x;
+  else if (j < 8) v.y = (v.y & m) | x;
+  else if (j < 12) v.z = (v.z & m) | x;
+  else v.w = (v.w & m) | x;
+  return v;
+}
+
+// Masked LE sum of the chunk's bytes at packet positions [lo, hi) (chunk at x0).
+__device__ __forceinline__ uint64_t chunk_sum(const uint4& v, int x0, int lo, int hi) {
+  if (x0 >= lo && x0 + 16 <= hi) return (uint64_t)v.x + v.y + v.z + v.w;
+  const uint32_t m16 = byte_bits16(lo - x0, hi - x0);
+  return (uint64_t)(v.x & expand_nibble(m16 & 0xF)) + (v.y & expand_nibble((m16 >> 4) & 0xF)) +
+         (v.z & expand_nibble((m16 >> 8) & 0xF)) + (v.w & expand_nibble((m16 >> 12) & 0xF));
+}
+
+// Store the part of a destination chunk that lies in [0, pkt_len).
+__device__ __forceinline__ void store_chunk(uint8_t* dchunk, const uint4& v, int x0, int pkt_len) {
+  if (x0 >= 0 && x0 + 16 <= pkt_len) {
+    *reinterpret_cast<uint4*>(dchunk) = v;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int x = x0 + j;
+      if (x >= 0 && x < pkt_len) dchunk[j] = (uint8_t)chunk_byte(v, j);
+    }
+  }
+}
+
+// Copy source positions -> destination chunks [k_begin, k_end) of a packet
+// whose byte x lives at src0 + x (source bytes valid in [src_lo, src_hi)),
+// destination chunk k covering packet positions [16k - dalign, +16).  Sums the
+// bytes at positions [sum_lo, pkt_len) into acc; optionally overrides the two
+// bytes at [pf, pf+2) with the big-endian value pv.
+template <bool SUM>
+__device__ __forceinline__ void copy_tail(const uint4& a, const uint4& b, int s, int k, int k_end, int dalign,
+                                          int pkt_len, int sum_lo, int pf, uint32_t pv, uint8_t* dbase,
+                                          uint64_t& acc) {
+  if (k < k_end) {
+    uint4 v = funnel(a, b, s);
+    const int x0 = 16 * k - dalign;
+    if (pf >= 0) {
+      const int j0 = pf - x0, j1 = pf + 1 - x0;
+      if (j0 >= 0 && j0 < 16) v = set_chunk_byte(v, j0, pv >> 8);
+      if (j1 >= 0 && j1 < 16) v = set_chunk_byte(v, j1, pv);
+    }
+    if (SUM) acc += chunk_sum(v, x0, sum_lo, pkt_len);
+    store_chunk(dbase + 16 * k, v, x0, pkt_len);
+  }
+}
+
+__device__ __forceinline__ void neighbour(const uint4& a, uint4& b, const uint8_t* ca, const uint8_t* src_lo,
+                                          const uint8_t* src_hi, int lane) {
+  b.x = __shfl_down(a.x, 1);
+  b.y = __shfl_down(a.y, 1);
+  b.z = __shfl_down(a.z, 1);
+  b.w = __shfl_down(a.w, 1);
+  if (lane == 63) {
+    const uint8_t* cb = ca + 16;
+    b = make_uint4(0, 0, 0, 0);
+    if (cb < src_hi && cb + 16 > src_lo) b = ld16(cb);
+  }
+}
+
+// Copy source positions -> destination chunks [k_begin, k_end) of a packet
+// whose byte x lives at src0 + x (source bytes valid in [src_lo, src_hi)),
+// destination chunk k covering packet positions [16k - dalign, +16).  Sums the
+// bytes at positions [sum_lo, pkt_len) into acc; optionally overrides the two
+// bytes at [pf, pf+2) with the big-endian value pv.  Two 64-chunk iterations
+// are loaded before either is consumed (2 KiB in flight per wave).
+template <bool SUM>
+__device__ __forceinline__ void stream_copy(const uint8_t* src0, const uint8_t* src_lo, const uint8_t* src_hi,
+                                            uint8_t* dbase, int dalign, int k_begin, int k_end, int pkt_len,
+                                            int sum_lo, int pf, uint32_t pv, int lane, uint64_t& acc) {
+  const uint8_t* w0 = src0 - dalign;  // source address of dest chunk 0's first byte
+  const int s = (int)((uintptr_t)w0 & 15);
+  const uint8_t* abase = w0 - s;
+  for (int k0 = k_begin; k0 < k_end; k0 += 128) {
+    const int ka = k0 + lane, kb = k0 + 64 + lane;
+    const uint8_t* ca = abase + 16 * (long)ka;
+    const uint8_t* cb = abase + 16 * (long)kb;
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = make_uint4(0, 0, 0, 0);
+    if (ca < src_hi && ca + 16 > src_lo) a0 = ld16(ca);
+    if (k0 + 64 < k_end && cb < src_hi && cb + 16 > src_lo) a1 = ld16(cb);
+    uint4 b0, b1;
+    neighbour(a0, b0, ca, src_lo, src_hi, lane);
+    copy_tail<SUM>(a0, b0, s, ka, k_end, dalign, pkt_len, sum_lo, pf, pv, dbase, acc);
+    if (k0 + 64 < k_end) {  // wave-uniform
+      neighbour(a1, b1, cb, src_lo, src_hi, lane);
+      copy_tail<SUM>(a1, b1, s, kb, k_end, dalign, pkt_len, sum_lo, pf, pv, dbase, acc);
+    }
+  }
+}
+
+// dst[0:n) = src[0:n), any alignments (no checksum).
+__device__ __forceinline__ void copy_range(const uint8_t* src, int n, uint8_t* dst, int lane) {
+  if (n <= 0) return;
+  const int dalign = (int)((uintptr_t)dst & 15);
+  const int nk = (n + dalign + 15) >> 4;
+  uint64_t unused = 0;
+  stream_copy<false>(src, src, src + n, dst - dalign, dalign, 0, nk, n, n, -1, 0, lane, unused);
+}
+
+}  // namespace wgcs

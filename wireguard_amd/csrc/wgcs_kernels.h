@@ -12,7 +12,7 @@ struct LaunchTuning {
   int blocks_per_cu = 8;   // 256-thread blocks per CU for the persistent grid
   int lanes_per_pkt = 16;  // 16: one DPP row per packet (4 per wave); 64: one wave per packet
   int unroll = 6;          // 16-byte loads in flight per lane per iteration
-  int nt = 0;              // non-temporal (streaming) loads
+  int nt = 1;              // non-temporal (streaming) loads: each byte is read once
 };
 
 hipError_t launch_checksum_batch(int mode, unsigned flags, uint8_t* arena, const wgcs_pkt* pkts,
@@ -23,5 +23,24 @@ hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs
                                   uint8_t* out, uint32_t out_stride, uint32_t offset, uint32_t max_segs,
                                   int32_t* sizes, int32_t* count, int32_t* status, hipStream_t s,
                                   int num_cu);
+
+// One coalesced GRO output (applyTCPCoalesce / applyUDPCoalesce item).
+struct GroItem {
+  uint64_t out_off;   // [10-byte virtio header | packet] written at out + out_off
+  uint32_t head_off;  // stage offset of the head packet (header source)
+  uint32_t pkt_len;   // final IP packet length
+  uint32_t seg_first, seg_count;  // payload segments in segs[]
+  uint16_t gso_size;
+  uint8_t iph, l4h;
+  uint8_t kind;  // GRO_KIND_*
+  uint8_t pad[7];
+};
+struct GroSeg {
+  uint32_t src_off, len;  // stage offset / length of one payload piece
+};
+enum : uint8_t { GRO_KIND_V6 = 1, GRO_KIND_UDP = 2, GRO_KIND_PSH = 4 };
+
+hipError_t launch_gro_coalesce(const uint8_t* stage, const GroItem* items, uint32_t n_items, const GroSeg* segs,
+                               uint8_t* out, hipStream_t s, int num_cu);
 
 }  // namespace wgcs
