@@ -2,18 +2,19 @@
 """bench.py -- device-resident Internet-checksum throughput on MI355X.
 
 Metric (BASELINE.json): "device-resident payload GiB/s, Internet checksum,
-64k×1500B batch".  One step = one pass of the hot path (one kernel launch of
+64k×1500B batch".  One step = one pass of the hot path (one launch of
 WGCS_MODE_VALIDATE = checksumValid, /root/reference/tun/gro.go:554-612) over
 one batch of 65,536 × 1500-B TCP/IPv4 frames already resident in HBM.  Payload
 bytes = sum of frame lengths (every byte of a frame is read: addresses for the
 pseudo-header, the L4 header and the payload).
 
-Contract: `python bench.py --gpus N --steps K --warmup W`; for N>1 it is run
-under torch.distributed.run, one rank per GPU.  Each rank checksums its own
-batch (weak scaling, no data-path collective -- per-packet checksums are
-independent).  The timed region is bracketed by a barrier +
-device sync on both sides; the max time over ranks is used; rank 0 prints ONE
-JSON line.
+Contract: `python bench.py --gpus N --steps K --warmup W`; for N>1 it runs
+under torch.distributed.run, one rank per GPU.  Default config (cfg2): each
+rank checksums its own 64k batch (weak scaling, no data-path collective --
+per-packet checksums are independent).  --config cfg5 runs
+the 1,048,576-frame mixed batch split across the ranks (strong scaling).  The
+timed region is bracketed by a barrier + device sync on both sides; the max
+time over ranks is used; rank 0 prints ONE JSON line.
 
 Infinity Cache: a 98.3 MB batch fits the 256 MiB MALL, so the bench rotates
 over R distinct copies (default 4 = 393 MB) so every launch reads HBM.
@@ -32,12 +33,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
 CONFIGS = {
-    # name: (n_packets, frame_len, kinds, BASELINE.json configs index)
-    "cfg2": (65536, 1500, "tcp4", 1),
-    "cfg3": (65536, 9000, "tcp4", 2),
-    "cfg5": (131072, 1500, "mixed", 4),  # per-GPU shard of 1,048,576 mixed frames at 8 GPUs
+    # name: (packets, frame_len, kinds, BASELINE.json configs index, scaling)
+    "cfg2": (65536, 1500, "tcp4", 1, "weak"),
+    "cfg3": (65536, 9000, "tcp4", 2, "weak"),
+    "cfg5": (1048576, 1500, "mixed", 4, "strong"),  # global batch, split across the ranks
 }
 
 
@@ -51,32 +53,31 @@ def parse():
     ap.add_argument("--rotate", type=int, default=4, help="distinct batch copies (defeat the 256 MiB MALL)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-event-timing", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end measurement")
     ap.add_argument("--verify", action="store_true", help="check the GPU results against the synth ground truth")
     return ap.parse_args()
 
 
 def main():
     args = parse()
-    import torch
+    import torch  # before wireguard_amd: one HIP runtime per process
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from wireguard_amd import shard, synth
+    from wireguard_amd.tun import Device, MODE_VALIDATE, MODE_L4_FILL
+
+    world, rank, local = shard.dist_env()
+    dist = None
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
-        dist = None
         torch.cuda.set_device(0)
 
     def barrier():
         if dist is not None:
             dist.barrier()
-
-    from wireguard_amd import synth
-    from wireguard_amd.tun import Device, MODE_VALIDATE, MODE_L4_FILL
 
     dev = Device(local if world > 1 else 0)
     if args.config == "cfg4":
@@ -84,20 +85,23 @@ def main():
 
         return gso_bench.run(args, torch, dev, dist, rank, world, local, barrier)
 
-    n, flen, kinds, cfg_idx = CONFIGS[args.config]
+    n_cfg, flen, kinds, cfg_idx, scaling = CONFIGS[args.config]
     mode = MODE_VALIDATE if args.mode == "validate" else MODE_L4_FILL
-    # each rank gets its own seeded shard (weak scaling)
-    arena_np, pkts_np, _ = synth.make_batch(n, flen, kinds=kinds, seed=synth.SEED + rank)
+    if scaling == "strong":
+        arena_np, pkts_np, _, lo, hi = shard.make_global_shard(n_cfg, rank, world, flen, kinds)
+    else:  # every rank its own seeded 64k batch
+        arena_np, pkts_np, _ = synth.make_batch(n_cfg, flen, kinds=kinds, seed=synth.SEED + rank)
+    n = len(pkts_np)
     bytes_per_step = int(pkts_np["len"].astype(np.int64).sum())
     stream = torch.cuda.Stream()  # dedicated stream: kernel launches and events share it
-    arenas = [torch.from_numpy(arena_np).to("cuda") for _ in range(args.rotate)]
+    R = args.rotate if bytes_per_step * args.rotate > (300 << 20) else max(args.rotate, (400 << 20) // bytes_per_step)
+    arenas = [torch.from_numpy(arena_np).to("cuda") for _ in range(R)]
     pkts = torch.from_numpy(pkts_np.view(np.uint8)).to("cuda")
-    outs = [torch.empty(n, dtype=torch.uint8 if mode == MODE_VALIDATE else torch.int16, device="cuda")
-            for _ in range(args.rotate)]
+    outs = [torch.empty(n * 2, dtype=torch.uint8, device="cuda") for _ in range(R)]
     torch.cuda.synchronize()
 
     def step(k):
-        i = k % args.rotate
+        i = k % R
         dev.checksum_batch(mode, arenas[i], pkts, n, outs[i], stream=stream)
 
     for k in range(args.warmup):
@@ -105,17 +109,16 @@ def main():
     torch.cuda.synchronize()
     if args.verify:
         if mode == MODE_VALIDATE:
-            assert bool(outs[0].all().item()), "VALIDATE: synthetic frames must all be valid"
-        else:
-            # L4 fill of a valid frame reproduces the stored checksum field
-            got = outs[0].cpu().numpy().view(np.uint16)
+            assert bool(outs[0][:n].all().item()), "VALIDATE: synthetic frames must all be valid"
+        else:  # L4 fill of a valid frame reproduces the stored checksum field
+            got = outs[0].cpu().numpy().view(np.uint16)[:n]
             a = arena_np[: n * flen].reshape(n, flen)
             cs = pkts_np["csum_start"].astype(np.int64) + pkts_np["csum_offset"]
             want = (a[np.arange(n), cs].astype(np.uint16) << 8) | a[np.arange(n), cs + 1]
             assert np.array_equal(got, want), "L4_FILL mismatch vs stored checksums"
 
     # HIP events on the launch stream bracket the timed region (one pair: an
-    # event between launches would add a ~10 µs gap per step); launches are
+    # event between launches would add a ~10 us gap per step); launches are
     # back-to-back on one stream, so elapsed / steps = the average launch
     # duration rocprofv3 reports for the kernel (profiles/).
     use_events = not args.no_event_timing
@@ -132,16 +135,15 @@ def main():
         e1.record(stream)
     torch.cuda.synchronize()
     barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    elapsed = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / args.steps if use_events else None
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # timing only, not on the data path
-        elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(elapsed, dist, device="cuda")
 
-    total_bytes = bytes_per_step * args.steps * world
+    total_bytes = bytes_per_step * args.steps * world  # every rank processed bytes_per_step per step
+    if scaling == "strong":
+        total_bytes = int(n_cfg) * flen * args.steps
     value = total_bytes / elapsed / 2**30
+    kname = "checksum_batch_kernel<VALIDATE,16,6,nt>" if mode == MODE_VALIDATE else "checksum_batch_kernel<L4_FILL,16,6,nt>"
     result = {
         "metric": "device-resident payload GiB/s, Internet checksum, 64k×1500B batch",
         "value": round(value, 2),
@@ -151,18 +153,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
         "config": {
-            "workload": f"{n} x {flen}-B {kinds} frames per GPU, {args.mode} (checksumValid) per step, "
-                        f"BASELINE.json configs[{cfg_idx}]",
+            "workload": (f"{n} x {flen}-B {kinds} frames per GPU" if scaling == "weak" else
+                         f"{n_cfg} x {flen}-B {kinds} frames split over {world} GPU(s)") +
+                        f", {args.mode} (checksumValid) per step, BASELINE.json configs[{cfg_idx}]",
             "packets_per_gpu": n,
             "frame_len": flen,
-            "global_batch_bytes": bytes_per_step * world,
+            "global_batch_bytes": bytes_per_step * world if scaling == "weak" else n_cfg * flen,
             "mode": args.mode,
-            "rotated_copies": args.rotate,
+            "rotated_copies": R,
             "parallelism": f"shard{world} (no collective)",
         },
     }
@@ -174,11 +177,15 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
-            "kernel": "checksum_batch_kernel<VALIDATE>" if mode == MODE_VALIDATE else "checksum_batch_kernel<L4_FILL>",
+            "traffic": traffic_per_launch(kname, bytes_per_step),
+            "kernel": kname,
             "kernel_ms": round(kern_ms, 5),
             "algorithmic_bytes_per_launch": bytes_per_step,
+            "algorithmic_bytes_per_unit": flen,
+            "units_per_launch": n,
         }
+    if rank == 0 and world == 1 and not args.no_e2e:
+        result["end_to_end"] = end_to_end(torch, dev, arena_np, pkts_np, mode, stream)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(arena_np, pkts_np, mode, args.cpu_seconds)
     if rank == 0:
@@ -186,6 +193,47 @@ def main():
     dev.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def traffic_per_launch(kname, algo_bytes):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass
+    (profiles/traffic.json, written by scripts/pmc_traffic.py from
+    FETCH_SIZE x 2 x 1024 + WRITE_SIZE x 1024, MI355X_MICROARCH.md §HBM)."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+        rec = t.get(kname)
+        if rec and rec.get("algorithmic_bytes") == algo_bytes:
+            return rec["hbm_bytes_per_launch"]
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def end_to_end(torch, dev, arena_np, pkts_np, mode, stream, iters=20):
+    """Host -> device -> host rate: pinned H2D of the batch, the kernel, D2H of
+    the per-packet results (the path starts and ends in host memory, tun/tun.go:490,:688)."""
+    n = len(pkts_np)
+    nbytes = int(pkts_np["len"].astype(np.int64).sum())
+    h_arena = torch.from_numpy(arena_np).pin_memory()
+    h_out = torch.empty(n * 2, dtype=torch.uint8).pin_memory()
+    d_arena = torch.empty(len(arena_np), dtype=torch.uint8, device="cuda")
+    d_pkts = torch.from_numpy(pkts_np.view(np.uint8)).to("cuda")
+    d_out = torch.empty(n * 2, dtype=torch.uint8, device="cuda")
+    out_b = n if mode == 2 else 2 * n
+    with torch.cuda.stream(stream):
+        for it in range(iters + 3):
+            if it == 3:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            d_arena.copy_(h_arena, non_blocking=True)
+            dev.checksum_batch(mode, d_arena, d_pkts, n, d_out, stream=stream)
+            h_out[:out_b].copy_(d_out[:out_b], non_blocking=True)
+        torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    return {"value": round(nbytes / dt / 2**30, 2), "unit": "GiB/s", "ms_per_batch": round(dt * 1e3, 4),
+            "what": "pinned H2D of the batch + kernel + D2H of the per-packet results, serialized on one "
+                    "stream (PCIe Gen5 x16 bound)"}
 
 
 def cpu_baseline(arena_np, pkts_np, mode, seconds):

@@ -58,24 +58,31 @@ __device__ __forceinline__ uint64_t chunk_sum(const uint4& v, int x0, int lo, in
          (v.z & expand_nibble((m16 >> 8) & 0xF)) + (v.w & expand_nibble((m16 >> 12) & 0xF));
 }
 
-// Store the part of a destination chunk that lies in [0, pkt_len).
+// Store the part of a destination chunk that lies in [0, pkt_len): full
+// chunks as one dwordx4; a partial chunk [lo, hi) as naturally aligned
+// byte/short/dword/dwordx2 pieces (at most 7 stores instead of 16 bytes).
 __device__ __forceinline__ void store_chunk(uint8_t* dchunk, const uint4& v, int x0, int pkt_len) {
   if (x0 >= 0 && x0 + 16 <= pkt_len) {
     *reinterpret_cast<uint4*>(dchunk) = v;
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int x = x0 + j;
-      if (x >= 0 && x < pkt_len) dchunk[j] = (uint8_t)chunk_byte(v, j);
-    }
+    return;
   }
+  int p = max(-x0, 0);
+  const int hi = min(pkt_len - x0, 16);
+  if (p >= hi) return;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  auto dw = [&](int q) { return w[q >> 2]; };
+  if ((p & 1) && p < hi) { dchunk[p] = (uint8_t)(dw(p) >> (8 * (p & 3))); p += 1; }
+  if ((p & 2) && p + 2 <= hi) { *reinterpret_cast<uint16_t*>(dchunk + p) = (uint16_t)(dw(p) >> (8 * (p & 3))); p += 2; }
+  if ((p & 4) && p + 4 <= hi) { *reinterpret_cast<uint32_t*>(dchunk + p) = dw(p); p += 4; }
+  if (p + 8 <= hi) {  // p is 0 or 8 here
+    *reinterpret_cast<uint2*>(dchunk + p) = make_uint2(dw(p), dw(p + 4));
+    p += 8;
+  }
+  if (p + 4 <= hi) { *reinterpret_cast<uint32_t*>(dchunk + p) = dw(p); p += 4; }
+  if (p + 2 <= hi) { *reinterpret_cast<uint16_t*>(dchunk + p) = (uint16_t)(dw(p) >> (8 * (p & 3))); p += 2; }
+  if (p < hi) dchunk[p] = (uint8_t)(dw(p) >> (8 * (p & 3)));
 }
 
-// Copy source positions -> destination chunks [k_begin, k_end) of a packet
-// whose byte x lives at src0 + x (source bytes valid in [src_lo, src_hi)),
-// destination chunk k covering packet positions [16k - dalign, +16).  Sums the
-// bytes at positions [sum_lo, pkt_len) into acc; optionally overrides the two
-// bytes at [pf, pf+2) with the big-endian value pv.
 template <bool SUM>
 __device__ __forceinline__ void copy_tail(const uint4& a, const uint4& b, int s, int k, int k_end, int dalign,
                                           int pkt_len, int sum_lo, int pf, uint32_t pv, uint8_t* dbase,
@@ -133,6 +140,56 @@ __device__ __forceinline__ void stream_copy(const uint8_t* src0, const uint8_t* 
       neighbour(a1, b1, cb, src_lo, src_hi, lane);
       copy_tail<SUM>(a1, b1, s, kb, k_end, dalign, pkt_len, sum_lo, pf, pv, dbase, acc);
     }
+  }
+}
+
+// First 128 destination chunks of a stream_copy, split into an early load
+// phase (issue the HBM loads, keep them in flight) and a later store phase,
+// so independent work (GSO header assembly) hides the load latency.
+struct CopyBatch {
+  uint4 a0, a1, e0, e1;  // own chunks and lane 63's next chunks
+  const uint8_t* abase;
+  int s, k0;
+};
+
+__device__ __forceinline__ CopyBatch copy_batch_load(const uint8_t* src0, const uint8_t* src_lo, const uint8_t* src_hi,
+                                                     int dalign, int k_begin, int k_end, int lane) {
+  CopyBatch B;
+  const uint8_t* w0 = src0 - dalign;
+  B.s = (int)((uintptr_t)w0 & 15);
+  B.abase = w0 - B.s;
+  B.k0 = k_begin;
+  const uint8_t* ca = B.abase + 16 * (long)(k_begin + lane);
+  const uint8_t* cb = ca + 64 * 16;
+  B.a0 = B.a1 = B.e0 = B.e1 = make_uint4(0, 0, 0, 0);
+  if (k_begin < k_end && ca < src_hi && ca + 16 > src_lo) B.a0 = ld16(ca);
+  if (k_begin + 64 < k_end && cb < src_hi && cb + 16 > src_lo) B.a1 = ld16(cb);
+  if (lane == 63) {
+    if (ca + 16 < src_hi && ca + 32 > src_lo) B.e0 = ld16(ca + 16);
+    if (k_begin + 64 < k_end && cb + 16 < src_hi && cb + 32 > src_lo) B.e1 = ld16(cb + 16);
+  }
+  return B;
+}
+
+template <bool SUM>
+__device__ __forceinline__ void copy_batch_store(const CopyBatch& B, uint8_t* dbase, int dalign, int k_end, int pkt_len,
+                                                 int sum_lo, int lane, uint64_t& acc) {
+  if (B.k0 >= k_end) return;
+  uint4 b0;
+  b0.x = __shfl_down(B.a0.x, 1);
+  b0.y = __shfl_down(B.a0.y, 1);
+  b0.z = __shfl_down(B.a0.z, 1);
+  b0.w = __shfl_down(B.a0.w, 1);
+  if (lane == 63) b0 = B.e0;
+  copy_tail<SUM>(B.a0, b0, B.s, B.k0 + lane, k_end, dalign, pkt_len, sum_lo, -1, 0, dbase, acc);
+  if (B.k0 + 64 < k_end) {  // wave-uniform
+    uint4 b1;
+    b1.x = __shfl_down(B.a1.x, 1);
+    b1.y = __shfl_down(B.a1.y, 1);
+    b1.z = __shfl_down(B.a1.z, 1);
+    b1.w = __shfl_down(B.a1.w, 1);
+    if (lane == 63) b1 = B.e1;
+    copy_tail<SUM>(B.a1, b1, B.s, B.k0 + 64 + lane, k_end, dalign, pkt_len, sum_lo, -1, 0, dbase, acc);
   }
 }
 
