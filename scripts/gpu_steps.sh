@@ -34,9 +34,9 @@ for s in "$@"; do
     bench-cfg3) step bench_cfg3 300 python bench.py --config cfg3 --steps 100 --warmup 10 --cpu-seconds 0 ;;
     bench-cfg4) step bench_cfg4 300 python bench.py --config cfg4 --steps 100 --warmup 10 --cpu-seconds 0 ;;
     bench-cfg5) step bench_cfg5 300 python bench.py --config cfg5 --steps 100 --warmup 10 --cpu-seconds 0 ;;
-    prof) (cd /tmp && step prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0) ;;
-    pmc) (cd /tmp && step pmc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-event-timing) ;;
-    pmc-w) (cd /tmp && step pmcw 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-event-timing) ;;
+    prof) (cd /tmp && step prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e) ;;
+    pmc) (cd /tmp && step pmc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e --no-event-timing) ;;
+    pmc-w) (cd /tmp && step pmcw 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e --no-event-timing) ;;
     prof-cfg4) (cd /tmp && step prof_cfg4 400 rocprofv3 --kernel-trace --stats -d "$OUT/profcfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 50 --warmup 5 --cpu-seconds 0) ;;
     pmc-sq-cfg4) (cd /tmp && step pmcsq_cfg4 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD --kernel-trace -d "$OUT/pmcsqcfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 20 --warmup 2 --cpu-seconds 0) ;;
     pmc-sq) (cd /tmp && step pmcsq 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD --kernel-trace -d "$OUT/pmcsq_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --cpu-seconds 0) ;;

@@ -27,6 +27,7 @@ struct GsoResult {
 
 // Runs one job through the kernel with bufs as the output slots.
 // vbuf = [10-byte virtio header | packet bytes] in host memory.
+// Caller holds ctx->mu (vbuf may be the context's own pinned staging).
 int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflags, uint8_t* const* bufs,
                  const size_t* buf_lens, int nbufs, int* sizes, int offset, GsoResult* res) {
   if (nbufs <= 0 || !bufs || !buf_lens || !sizes || offset < 0)
@@ -36,7 +37,6 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   // Device slots mirror bufs[0]'s capacity (the reference's room check for
   // GSO_NONE is against bufs[0]); other buffers are checked after the kernel.
   const size_t stride = std::min<size_t>(buf_lens[0], (size_t)offset + std::max<size_t>(vlen, 16));
-  std::lock_guard<std::mutex> g(ctx->mu);
   hipSetDevice(ctx->device);
   int rc;
   const size_t meta = (size_t)nbufs * 4 + 16;
@@ -122,10 +122,8 @@ int wgcs_gso_split(wgcs_ctx* ctx, uint8_t* read_buf, size_t len, const wgcs_virt
   if (!ctx || !hdr || !n_out || (!read_buf && len)) return WGCS_ERR_INVALID_ARG;
   *n_out = 0;
   int rc;
-  {
-    std::lock_guard<std::mutex> g(ctx->mu);
-    if ((rc = ensure_pinned(ctx, ctx->h_out, len + 10))) return rc;
-  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if ((rc = ensure_pinned(ctx, ctx->h_out, len + 10))) return rc;
   uint8_t* v = (uint8_t*)ctx->h_out.ptr;
   v[0] = hdr->flags;
   v[1] = hdr->gso_type;
@@ -154,6 +152,7 @@ int wgcs_handle_virtio_read(wgcs_ctx* ctx, uint8_t* read_buf, size_t n, uint8_t*
   if (!ctx || !n_out || (!read_buf && n)) return WGCS_ERR_INVALID_ARG;
   *n_out = 0;
   GsoResult r;
+  std::lock_guard<std::mutex> g(ctx->mu);
   int rc = run_gso_host(ctx, read_buf, n, 0, bufs, buf_lens, nbufs, sizes, offset, &r);
   if (rc) return rc;
   if (n >= 10 && (r.status == 0 || r.status == WGCS_ERR_TOO_MANY_SEGMENTS)) {
