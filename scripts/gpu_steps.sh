@@ -24,6 +24,8 @@ for s in "$@"; do
   case $s in
     tests) step tests 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     tests-all) step tests 1100 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    tests-gso) step tests_gso 600 python -m pytest tests/test_gpu_gso.py tests/test_golden.py -m gpu -q -p no:cacheprovider ;;
+    bench-cfg4-legacy) step bench_cfg4_legacy 300 env WGCS_GSO_IMPL=1 python bench.py --config cfg4 --steps 100 --warmup 10 --cpu-seconds 0 ;;
     sweep) step sweep 400 python scripts/sweep_checksum.py ;;
     sweep-cfg3) step sweep_cfg3 400 python scripts/sweep_checksum.py --config cfg3 ;;
     probe) step probe 400 python scripts/probe_stream.py ;;
@@ -38,7 +40,8 @@ for s in "$@"; do
     pmc) (cd /tmp && step pmc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e --no-event-timing) ;;
     pmc-w) (cd /tmp && step pmcw 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e --no-event-timing) ;;
     prof-cfg4) (cd /tmp && step prof_cfg4 400 rocprofv3 --kernel-trace --stats -d "$OUT/profcfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 50 --warmup 5 --cpu-seconds 0) ;;
-    pmc-sq-cfg4) (cd /tmp && step pmcsq_cfg4 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD --kernel-trace -d "$OUT/pmcsqcfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 20 --warmup 2 --cpu-seconds 0) ;;
+    pmc-sq-cfg4) (cd /tmp && step pmcsq_cfg4 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace -d "$OUT/pmcsqcfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 20 --warmup 2 --cpu-seconds 0) ;;
+    pmc-sq2-cfg4) (cd /tmp && step pmcsq2_cfg4 400 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcsq2cfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 20 --warmup 2 --cpu-seconds 0) ;;
     pmc-sq) (cd /tmp && step pmcsq 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD --kernel-trace -d "$OUT/pmcsq_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --cpu-seconds 0) ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -11,7 +11,7 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libwgcsum.so")
+LIB_PATH = os.environ.get("WGCS_LIB") or os.path.join(_HERE, "libwgcsum.so")  # WGCS_LIB: A/B builds
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "wgcsum.h")
 
 # status codes (include/wgcsum.h)

@@ -56,7 +56,7 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->d_aux.ptr, hjob, sizeof(wgcs_gso_job), hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemsetAsync(d_sizes, 0, meta, s);
   if (e != hipSuccess) return hip_fail(ctx, e, "H2D");
-  if ((rc = ensure_dev(ctx, ctx->d_ws, gso_workspace_bytes(1)))) return rc;
+  if (gso_workspace_bytes(1) && (rc = ensure_dev(ctx, ctx->d_ws, gso_workspace_bytes(1)))) return rc;
   e = launch_gso_split_batch((const uint8_t*)ctx->d_arena.ptr, (const wgcs_gso_job*)ctx->d_aux.ptr, 1,
                              (uint8_t*)ctx->d_out.ptr, (uint32_t)stride, (uint32_t)offset, (uint32_t)nbufs, d_sizes,
                              d_count, d_status, ctx->d_ws.ptr, s, ctx->num_cu);
@@ -109,7 +109,8 @@ int wgcs_gso_split_batch(wgcs_ctx* ctx, const uint8_t* d_arena, const wgcs_gso_j
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   if ((uint64_t)n_jobs * max_segs > 0xFFFFFFFFull) return set_err(ctx, WGCS_ERR_INVALID_ARG, "n_jobs*max_segs >= 2^32");
   // per-job plans live in a context workspace (grown here, never inside a capture)
-  int rc = ensure_dev(ctx, ctx->d_ws, gso_workspace_bytes(n_jobs));
+  const size_t ws = gso_workspace_bytes(n_jobs);
+  int rc = ws ? ensure_dev(ctx, ctx->d_ws, ws) : WGCS_OK;
   if (rc) return rc;
   hipError_t e = launch_gso_split_batch(d_arena, d_jobs, n_jobs, d_out, out_stride, offset, max_segs, d_sizes, d_count,
                                         d_status, ctx->d_ws.ptr, s, ctx->num_cu);

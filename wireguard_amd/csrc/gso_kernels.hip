@@ -23,6 +23,8 @@
 // 0 -> 0xFFFF substitution; ErrTooManySegments returns n = max_segs - 1.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "../../include/wgcsum.h"
 #include "wgcs_common.h"
 #include "wgcs_copy.h"
@@ -435,15 +437,373 @@ __global__ __launch_bounds__(256) void gso_split_kernel(const uint8_t* __restric
   }
 }
 
-size_t gso_workspace_bytes(uint32_t n_jobs) { return (size_t)n_jobs * (sizeof(GsoPlan) + kTplBytes); }
+// ---------------------------------------------------------------------------
+// Row-per-segment split (default path): one 16-lane DPP row per OUTPUT
+// segment, 4 segments per wave, 16 per 256-thread block; grid = (job, group
+// of 16 segments).  Every wave decodes its job from L2-resident header bytes
+// (no separate plan launch).  Per row:
+//   * lanes r < hk fetch the segment's header chunk (two aligned 16-B loads +
+//     funnel to the destination phase) -- issued first, L2 hits;
+//   * the payload streams with U 16-byte non-temporal loads per lane in
+//     flight; destination chunk k = r + 16u is assembled from source chunks k
+//     and k+1 (k+1 comes from the next lane via DPP row_ror:15) and a per-row
+//     funnel shift, summed (v_dot2) and stored as one dwordx4;
+//   * header lanes patch the header (gro.go:1419-1465), add the IPv4 header,
+//     L4 header and pseudo-address bytes to the row sums, and after two row
+//     reductions store the header chunks with both checksums filled in.
+// Each output byte is written exactly once, each input byte read once.
+
+// DPP row_ror:15 -- lane r of each 16-lane row receives lane (r + 1) & 15.
+__device__ __forceinline__ uint32_t row_next(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x12F, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint4 row_next4(const uint4& v) {
+  return make_uint4(row_next(v.x), row_next(v.y), row_next(v.z), row_next(v.w));
+}
+
+// Bytes [s, s + 16) of the 32-byte concatenation a|b, s per lane in [0, 16).
+__device__ __forceinline__ uint4 funnel_v(const uint4& a, const uint4& b, int s) {
+  // two select stages on plain values (no private arrays: a select between
+  // array elements becomes a dynamically indexed alloca -> scratch/LDS)
+  const bool q1 = (s & 4) != 0, q2 = (s & 8) != 0;
+  const uint32_t f0 = q1 ? a.y : a.x, f1 = q1 ? a.z : a.y, f2 = q1 ? a.w : a.z, f3 = q1 ? b.x : a.w;
+  const uint32_t f4 = q1 ? b.y : b.x, f5 = q1 ? b.z : b.y, f6 = q1 ? b.w : b.z;
+  const uint32_t e0 = q2 ? f2 : f0, e1 = q2 ? f3 : f1, e2 = q2 ? f4 : f2, e3 = q2 ? f5 : f3, e4 = q2 ? f6 : f4;
+  const int r = s & 3;
+  return make_uint4(__builtin_amdgcn_alignbyte(e1, e0, r), __builtin_amdgcn_alignbyte(e2, e1, r),
+                    __builtin_amdgcn_alignbyte(e3, e2, r), __builtin_amdgcn_alignbyte(e4, e3, r));
+}
+
+__device__ __forceinline__ uint32_t add4(uint32_t acc, const uint4& v) {
+  return add_halves(add_halves(add_halves(add_halves(acc, v.x), v.y), v.z), v.w);
+}
+
+// acc + the chunk's bytes selected by the 16-bit byte mask m16 (rot: the
+// range pairs bytes with the opposite parity of acc's range, wgcs_common.h).
+__device__ __forceinline__ uint32_t add4_masked(uint32_t acc, const uint4& v, uint32_t m16, bool rot) {
+  uint32_t y0 = v.x & expand_nibble(m16 & 0xFu), y1 = v.y & expand_nibble((m16 >> 4) & 0xFu);
+  uint32_t y2 = v.z & expand_nibble((m16 >> 8) & 0xFu), y3 = v.w & expand_nibble((m16 >> 12) & 0xFu);
+  if (rot) {
+    y0 = rotl8(y0);
+    y1 = rotl8(y1);
+    y2 = rotl8(y2);
+    y3 = rotl8(y3);
+  }
+  return add_halves(add_halves(add_halves(add_halves(acc, y0), y1), y2), y3);
+}
+
+// Per-byte select: bytes whose bit is set in m16 from a, the rest from b.
+__device__ __forceinline__ uint4 select_bytes(const uint4& a, const uint4& b, uint32_t m16) {
+  const uint32_t m0 = expand_nibble(m16 & 0xF), m1 = expand_nibble((m16 >> 4) & 0xF);
+  const uint32_t m2 = expand_nibble((m16 >> 8) & 0xF), m3 = expand_nibble((m16 >> 12) & 0xF);
+  return make_uint4((a.x & m0) | (b.x & ~m0), (a.y & m1) | (b.y & ~m1), (a.z & m2) | (b.z & ~m2),
+                    (a.w & m3) | (b.w & ~m3));
+}
+
+// Write byte value b at packet position pos into the chunk at position x0,
+// if pos < lim (header bytes only; the payload copy wins above hdrLen).
+__device__ __forceinline__ void put_byte(uint4& v, int x0, int pos, uint32_t b, int lim) {
+  const int t = pos - x0;
+  if (pos < lim && t >= 0 && t < 16) v = set_chunk_byte(v, t, b);
+}
+__device__ __forceinline__ void put_be16(uint4& v, int x0, int pos, uint32_t val, int lim) {
+  put_byte(v, x0, pos, val >> 8, lim);
+  put_byte(v, x0, pos + 1, val, lim);
+}
+
+template <bool NT>
+__device__ __forceinline__ uint4 ld_src(const uint8_t* p) {
+  if (NT) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(t.x, t.y, t.z, t.w);
+  }
+  return ld16(p);
+}
+
+// Job-uniform header sums for the common case ("fast" header): every
+// per-segment header write lands inside hdrLen at a position disjoint from the
+// L4 checksum field, so the per-segment IPv4 and L4 header sums are a job
+// constant plus the rewritten field values (no per-segment byte sums).
+struct HdrFast {
+  bool fast;
+  uint32_t ip_base;   // BE words of readBuf[0:csumStart) with [2:6) and [10:12) zero (IPv4)
+  uint32_t l4_base;   // BE words of readBuf[csumStart:hdrLen) pairing from csumStart, csum field and
+                      // seq / UDP-length zero, FIN|PSH cleared
+  uint32_t addr;      // BE words of the pseudo-header addresses
+  uint32_t flags;     // readBuf[csumStart + 13] (TCP flags byte)
+};
+
+__device__ __forceinline__ HdrFast header_fast(const HdrBytes& hb, const Job& j, int lane) {
+  HdrFast h;
+  const int cs = j.cs, hl = j.hdr_len, ca = (j.cs + j.co) & 0xFFFF;
+  const bool v4 = j.ipv == 4, tcp = j.type != GSO_UDP_L4;
+  const int vlo = cs + 4, vhi = tcp ? cs + 8 : cs + 6;  // per-segment L4 field bytes
+  h.fast = (tcp ? cs + 14 <= hl : vhi <= hl) && (ca + 2 <= vlo || ca >= vhi) &&
+           (!tcp || (ca != cs + 13 && ca + 1 != cs + 13));
+  const int a_lo = v4 ? 12 : 8, a_hi = v4 ? 20 : 40;
+  uint32_t ip = 0, l4 = 0, ad = 0;
+  const uint32_t regs[4] = {hb.r0, hb.r1, hb.r2, hb.r3};
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int x = lane + 64 * m - 10;  // readBuf position of this lane's byte
+    const uint32_t b = regs[m];
+    if (x < 0 || x >= hl) continue;
+    const uint32_t hi8 = b << 8;
+    if (v4 && x < cs && (x < 2 || x >= 6) && x != 10 && x != 11) ip += (x & 1) ? b : hi8;
+    if (x >= cs && x != ca && x != ca + 1 && (x < vlo || x >= vhi)) {
+      const uint32_t bb = (tcp && x == cs + 13) ? (b & ~0x09u) : b;
+      l4 += ((x - cs) & 1) ? bb : (bb << 8);
+    }
+    if (x >= a_lo && x < a_hi) ad += (x & 1) ? b : hi8;
+  }
+  h.ip_base = wave_sum_u32(ip);
+  h.l4_base = wave_sum_u32(l4);
+  h.addr = wave_sum_u32(ad);
+  h.flags = tcp ? hb(10 + cs + 13) : 0u;
+  return h;
+}
+
+// DPP row_shr:1 -- lane r of each row receives lane r - 1 (lane 0: zero).
+__device__ __forceinline__ uint4 row_prev4(const uint4& v) {
+  return make_uint4((uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.x, 0x111, 0xF, 0xF, false),
+                    (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.y, 0x111, 0xF, 0xF, false),
+                    (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.z, 0x111, 0xF, 0xF, false),
+                    (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.w, 0x111, 0xF, 0xF, false));
+}
+
+// Header chunks in packet coordinates (lane r: bytes [16r, 16r + 16)):
+// write byte / big-endian u16 `val` at the wave-uniform position pos.
+__device__ __forceinline__ void put_u(uint4& P, int r, int pos, uint32_t val, uint32_t nbytes_mask) {
+  const int sh = 8 * (pos & 3);
+  const uint32_t m = r == (pos >> 4) ? (nbytes_mask << sh) : 0u;
+  const uint32_t v = val << sh;
+  switch ((pos >> 2) & 3) {
+    case 0: P.x = (P.x & ~m) | (v & m); break;
+    case 1: P.y = (P.y & ~m) | (v & m); break;
+    case 2: P.z = (P.z & ~m) | (v & m); break;
+    default: P.w = (P.w & ~m) | (v & m); break;
+  }
+}
+__device__ __forceinline__ void put_be16_u(uint4& P, int r, int pos, uint32_t val) {
+  if ((pos & 1) == 0) {  // both bytes in one dword (pos & 3 is 0 or 2)
+    put_u(P, r, pos, bswap16(val & 0xFFFFu), 0xFFFFu);
+  } else {
+    put_u(P, r, pos, (val >> 8) & 0xFFu, 0xFFu);
+    put_u(P, r, pos + 1, val & 0xFFu, 0xFFu);
+  }
+}
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gso_rows_kernel(
+    const uint8_t* __restrict__ arena, const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
+    uint8_t* __restrict__ out, uint32_t out_stride, uint32_t offset, uint32_t room, int32_t* __restrict__ sizes,
+    int32_t* __restrict__ count, int32_t* __restrict__ status) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15;
+  const int wv = threadIdx.x >> 6;
+  const uint32_t jb = blockIdx.x;
+  const uint8_t* vb = arena + jobs[jb].off;
+  const uint32_t jlen = jobs[jb].len;
+  HdrBytes hb;
+  hb.load(vb, (int)min(jlen, 256u), lane);
+  const Job j = decode_job(hb, jlen, jobs[jb].flags, room, max_segs);
+  const bool ok = j.status == 0 || j.status == WGCS_ERR_TOO_MANY_SEGMENTS;
+  if (blockIdx.y == 0 && threadIdx.x == 0) {
+    count[jb] = ok ? j.count : 0;
+    status[jb] = j.status;
+  }
+  if (!ok) return;
+  const uint32_t seg0 = blockIdx.y * 16u + (uint32_t)wv * 4u;  // wave-uniform
+  const uint8_t* rb = vb + 10;
+  const uint64_t slot0 = (uint64_t)jb * max_segs;
+  if (j.type == GSO_NONE) {  // one packet: whole wave 0 of the job's first block
+    if (seg0 == 0) {
+      none_segment(rb, j, out + slot0 * out_stride + offset, lane);
+      if (lane == 0) sizes[slot0] = j.plen;
+    }
+    return;
+  }
+  if (seg0 >= (uint32_t)j.nseg) return;
+  // job-uniform header values, read across the wave while every lane is live
+  const bool v4 = j.ipv == 4, tcp = j.type != GSO_UDP_L4;
+  const uint32_t id0 = v4 ? hb.be16(10 + 4) : 0u;
+  const uint32_t seq0 = tcp ? hb.be32(10 + j.cs + 4) : 0u;
+  const HdrFast hf = header_fast(hb, j, lane);
+  const int i = (int)seg0 + (lane >> 4);
+  if (i >= j.nseg) return;  // whole rows retire; DPP below stays inside live rows
+
+  // ---- segment geometry (row-uniform)
+  const int hdr_len = j.hdr_len, cs = j.cs, plen = j.plen;
+  const int csum_at = (cs + j.co) & 0xFFFF;
+  const int seg_start = hdr_len + i * j.gso;
+  const int seg_end = min(plen, seg_start + j.gso);
+  const int seg_len = seg_end - seg_start;
+  const int pkt_len = hdr_len + seg_len;
+  const bool last = seg_end == plen;
+  const uint64_t slot = slot0 + (uint32_t)i;
+  uint8_t* dst = out + slot * out_stride + offset;
+  const int dalign = (int)((uintptr_t)dst & 15u);
+  uint8_t* dbase = dst - dalign;
+  const int nk = (pkt_len + dalign + 15) >> 4;
+  const int hk = min((hdr_len + dalign + 15) >> 4, nk);
+  const uint8_t* w0 = rb + i * j.gso - dalign;  // source of destination chunk 0 (payload positions)
+  const int s = (int)((uintptr_t)w0 & 15u);
+  const uint8_t* abase = w0 - s;
+  const uint8_t* src_lo = rb + seg_start;
+  const uint8_t* src_hi = rb + seg_end;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+
+  // ---- header source loads first (shared by the job's segments: L2 hits).
+  // fast: packet coordinates (lane r = readBuf[16r, 16r + 16), wave-uniform
+  // phase); general: destination coordinates (per-row phase).
+  const uint8_t* hend = rb + hdr_len;
+  const int hph = hf.fast ? (int)((uintptr_t)rb & 15u) : (int)((uintptr_t)(rb - dalign) & 15u);
+  const uint8_t* hab = (hf.fast ? rb : rb - dalign) - hph + 16 * r;
+  uint4 H0 = z, H1 = z;
+  if (r < hk) {
+    if (hab < hend && hab + 16 > rb) H0 = ld16(hab);
+    if (hab + 16 < hend && hab + 32 > rb) H1 = ld16(hab + 16);
+  }
+
+  // ---- payload stream
+  uint32_t acc = 0;  // L4 bytes [hdrLen, pktLen): LE words at destination addresses
+  uint4 keep = z;    // payload part of header chunk r (r < hk)
+  for (int k0 = 0; k0 < nk; k0 += 16 * U) {
+    uint4 A[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint8_t* ca = abase + 16 * (k0 + r + 16 * u);
+      A[u] = (ca < src_hi && ca + 16 > src_lo) ? ld_src<NT>(ca) : z;
+    }
+    uint4 E = z;
+    if (r == 15) {
+      const uint8_t* ce = abase + 16 * (k0 + 16 * U);
+      if (ce < src_hi && ce + 16 > src_lo) E = ld_src<NT>(ce);
+    }
+    uint4 Rc = row_next4(A[0]);  // chunk k + 1 comes from the next lane (lane 15: lane 0's next u)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + r + 16 * u;
+      const uint4 Rx = u + 1 < U ? row_next4(A[u + 1 < U ? u + 1 : u]) : E;
+      const uint4 B = r == 15 ? Rx : Rc;
+      Rc = Rx;
+      if (k < nk) {
+        const uint4 v = funnel_v(A[u], B, s);
+        const int x0 = 16 * k - dalign;
+        if (x0 >= hdr_len && x0 + 16 <= pkt_len) acc = add4(acc, v);
+        else acc = add4_masked(acc, v, byte_bits16(hdr_len - x0, pkt_len - x0), false);
+        if (k < hk) keep = v;
+        else store_chunk(dbase + 16 * k, v, x0, pkt_len);
+      }
+    }
+  }
+
+  const uint32_t id = i > 0 ? ((id0 + 1) & 0xFFFFu) : id0;  // quirk: id0 + 1 for every i >= 1 (:1426-1431)
+  const uint32_t seq = seq0 + (uint32_t)(uint16_t)((uint16_t)j.gso * (uint16_t)i);  // uint16 product (:1445)
+  const uint32_t ulen = (uint32_t)(uint16_t)(seg_len + (hdr_len - cs));            // UDP length (:1462-1465)
+  const uint32_t tlen = (uint32_t)(uint16_t)(hdr_len - cs + seg_len);              // transportLen (:1469-1471)
+  const uint32_t proto = tcp ? 6u : 17u;
+  const int x0h = 16 * r - dalign;
+  const uint32_t hmask = byte_bits16(-x0h, hdr_len - x0h);  // header positions of destination chunk r
+
+  if (hf.fast) {
+    // ---- sums: payload (row reduction) + job constants + rewritten fields
+    uint32_t t_pay = fold32_16(row16_sum_u32(acc));
+    if ((((uintptr_t)dst + (uintptr_t)cs) & 1u) == 0) t_pay = bswap16(t_pay);  // pairing from csumStart
+    const uint32_t var = tcp ? (seq >> 16) + (seq & 0xFFFFu) + (last ? (hf.flags & 0x09u) : 0u) : ulen;
+    const uint32_t l4c = (~fold32_16(t_pay + fold32_16(hf.l4_base) + var + fold32_16(hf.addr) + proto + tlen)) & 0xFFFFu;
+    // ---- header chunk in packet coordinates, rewritten (gro.go:1418-1465, :1486-1490)
+    uint4 P = funnel(H0, H1, hph);
+    if (v4) {
+      const uint32_t ipc = (~fold32_16(fold32_16(hf.ip_base) + (uint32_t)pkt_len + id)) & 0xFFFFu;
+      put_be16_u(P, r, 2, (uint32_t)pkt_len);  // total length (:1433)
+      put_be16_u(P, r, 4, id);                 // identification (:1426-1431)
+      put_be16_u(P, r, 10, ipc);               // header checksum (:1434-1436)
+    } else {
+      put_be16_u(P, r, 4, (uint32_t)(pkt_len - cs));  // payload length (:1439)
+    }
+    if (tcp) {
+      put_be16_u(P, r, cs + 4, seq >> 16);  // sequence number (:1445-1446)
+      put_be16_u(P, r, cs + 6, seq);
+      put_u(P, r, cs + 13, last ? hf.flags : (hf.flags & ~0x09u), 0xFFu);  // FIN|PSH on the last only (:1447-1459)
+    } else {
+      put_be16_u(P, r, cs + 4, ulen);
+    }
+    put_be16_u(P, r, csum_at, l4c);  // L4 checksum (:1486-1490)
+    // ---- to destination phase, merge with the payload bytes, store
+    const uint4 Pp = row_prev4(P);
+    const uint4 D = dalign ? funnel_v(Pp, P, 16 - dalign) : P;
+    if (r < hk) store_chunk(dbase + 16 * r, select_bytes(D, keep, hmask), x0h, pkt_len);
+  } else {
+    // ---- general header path (unusual csum offsets / short RAW headers):
+    // byte-exact replay of the reference's write order on the chunk
+    const int a_lo = v4 ? 12 : 8, a_hi = v4 ? 20 : 40;
+    uint32_t acc_ip = 0;
+    uint4 hv = z;
+    if (r < hk) {
+      hv = select_bytes(funnel_v(H0, H1, hph), keep, hmask);
+      // readBuf's zeroed fields (gro.go:1388,:1393), then the per-segment header writes in order
+      if (v4) put_be16(hv, x0h, 10, 0, hdr_len);
+      put_be16(hv, x0h, csum_at, 0, hdr_len);
+      if (v4) {
+        put_be16(hv, x0h, 4, id, hdr_len);
+        put_be16(hv, x0h, 2, pkt_len, hdr_len);
+      } else {
+        put_be16(hv, x0h, 4, pkt_len - cs, hdr_len);
+      }
+      if (tcp) {
+        put_be16(hv, x0h, cs + 4, seq >> 16, hdr_len);
+        put_be16(hv, x0h, cs + 6, seq, hdr_len);
+        const int fl = cs + 13 - x0h;
+        if (!last && cs + 13 < hdr_len && fl >= 0 && fl < 16) hv = set_chunk_byte(hv, fl, chunk_byte(hv, fl) & ~0x09u);
+      } else {
+        put_be16(hv, x0h, cs + 4, ulen, hdr_len);
+      }
+      if (v4) acc_ip = add4_masked(0u, hv, byte_bits16(-x0h, cs - x0h), false);
+      acc = add4_masked(acc, hv, byte_bits16(cs - x0h, hdr_len - x0h), false);
+      acc = add4_masked(acc, hv, byte_bits16(a_lo - x0h, a_hi - x0h), (cs & 1) != 0);  // pseudo-header addresses
+    }
+    uint32_t t_ip = fold32_16(row16_sum_u32(acc_ip));
+    if ((((uintptr_t)dst) & 1u) == 0) t_ip = bswap16(t_ip);
+    uint32_t t_l4 = fold32_16(row16_sum_u32(acc));
+    if ((((uintptr_t)dst + (uintptr_t)cs) & 1u) == 0) t_l4 = bswap16(t_l4);
+    const uint32_t l4c = (~fold32_16(t_l4 + proto + tlen)) & 0xFFFFu;
+    if (r < hk) {
+      if (v4) put_be16(hv, x0h, 10, (~t_ip) & 0xFFFFu, hdr_len);
+      put_be16(hv, x0h, csum_at, l4c, hdr_len);
+      store_chunk(dbase + 16 * r, hv, x0h, pkt_len);
+    }
+  }
+  if (r == 0) sizes[slot] = pkt_len;
+}
+
+static int gso_impl() {
+  static int v = [] {
+    const char* e = getenv("WGCS_GSO_IMPL");  // 0 = row-per-segment (default), 1 = plan + wave-per-segment
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+size_t gso_workspace_bytes(uint32_t n_jobs) {
+  return gso_impl() == 1 ? (size_t)n_jobs * (sizeof(GsoPlan) + kTplBytes) : 0;
+}
 
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs, uint8_t* out,
                                   uint32_t out_stride, uint32_t offset, uint32_t max_segs, int32_t* sizes,
                                   int32_t* count, int32_t* status, void* workspace, hipStream_t s, int num_cu) {
   if (n_jobs == 0 || max_segs == 0) return hipSuccess;
+  const uint32_t room = out_stride > offset ? out_stride - offset : 0;
+  if (gso_impl() == 0) {
+    const uint32_t gy = (max_segs + 15) / 16;
+    if (gy > 65535u) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((gso_rows_kernel<6, true>), dim3(n_jobs, gy), dim3(256), 0, s, arena, jobs, max_segs, out,
+                       out_stride, offset, room, sizes, count, status);
+    return hipGetLastError();
+  }
   GsoPlan* plans = reinterpret_cast<GsoPlan*>(workspace);
   uint8_t* tpl = reinterpret_cast<uint8_t*>(plans + n_jobs);
-  const uint32_t room = out_stride > offset ? out_stride - offset : 0;
   uint32_t g1 = (n_jobs + 3) / 4;
   if (g1 > (uint32_t)num_cu * 8) g1 = (uint32_t)num_cu * 8;
   hipLaunchKernelGGL(gso_plan_kernel, dim3(g1), dim3(256), 0, s, arena, jobs, n_jobs, room, max_segs, plans, tpl,

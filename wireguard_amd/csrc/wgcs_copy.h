@@ -36,18 +36,26 @@ __device__ __forceinline__ uint4 funnel(const uint4& a, const uint4& b, int s) {
   return o;
 }
 
-__device__ __forceinline__ uint32_t chunk_byte(const uint4& v, int j) {
-  const uint32_t w = j < 4 ? v.x : (j < 8 ? v.y : (j < 12 ? v.z : v.w));
-  return (w >> (8 * (j & 3))) & 0xFFu;
+// Dynamic byte access goes through a 128-bit value (shifts and selects), never
+// through an indexed private array: a runtime index into one becomes an alloca
+// in scratch (or LDS) memory.
+typedef unsigned __int128 u128;
+__device__ __forceinline__ u128 to128(const uint4& v) {
+  return ((u128)(((uint64_t)v.w << 32) | v.z) << 64) | (((uint64_t)v.y << 32) | v.x);
+}
+__device__ __forceinline__ uint4 from128(u128 t) {
+  const uint64_t lo = (uint64_t)t, hi = (uint64_t)(t >> 64);
+  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
-__device__ __forceinline__ uint4 set_chunk_byte(uint4 v, int j, uint32_t b) {
-  const uint32_t sh = 8 * (j & 3), m = ~(0xFFu << sh), x = (b & 0xFFu) << sh;
-  if (j < 4) v.x = (v.x & m) | x;
-  else if (j < 8) v.y = (v.y & m) | x;
-  else if (j < 12) v.z = (v.z & m) | x;
-  else v.w = (v.w & m) | x;
-  return v;
+__device__ __forceinline__ uint32_t chunk_byte(const uint4& v, int j) {
+  return (uint32_t)(to128(v) >> (8 * j)) & 0xFFu;
+}
+
+__device__ __forceinline__ uint4 set_chunk_byte(const uint4& v, int j, uint32_t b) {
+  const int sh = 8 * j;
+  const u128 t = (to128(v) & ~((u128)0xFFu << sh)) | ((u128)(b & 0xFFu) << sh);
+  return from128(t);
 }
 
 // Masked LE sum of the chunk's bytes at packet positions [lo, hi) (chunk at x0).
@@ -69,18 +77,19 @@ __device__ __forceinline__ void store_chunk(uint8_t* dchunk, const uint4& v, int
   int p = max(-x0, 0);
   const int hi = min(pkt_len - x0, 16);
   if (p >= hi) return;
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  auto dw = [&](int q) { return w[q >> 2]; };
-  if ((p & 1) && p < hi) { dchunk[p] = (uint8_t)(dw(p) >> (8 * (p & 3))); p += 1; }
-  if ((p & 2) && p + 2 <= hi) { *reinterpret_cast<uint16_t*>(dchunk + p) = (uint16_t)(dw(p) >> (8 * (p & 3))); p += 2; }
-  if ((p & 4) && p + 4 <= hi) { *reinterpret_cast<uint32_t*>(dchunk + p) = dw(p); p += 4; }
+  const u128 t = to128(v);
+  auto at = [&](int q) { return (uint64_t)(t >> (8 * q)); };  // bytes [q, q + 8)
+  if ((p & 1) && p < hi) { dchunk[p] = (uint8_t)at(p); p += 1; }
+  if ((p & 2) && p + 2 <= hi) { *reinterpret_cast<uint16_t*>(dchunk + p) = (uint16_t)at(p); p += 2; }
+  if ((p & 4) && p + 4 <= hi) { *reinterpret_cast<uint32_t*>(dchunk + p) = (uint32_t)at(p); p += 4; }
   if (p + 8 <= hi) {  // p is 0 or 8 here
-    *reinterpret_cast<uint2*>(dchunk + p) = make_uint2(dw(p), dw(p + 4));
+    const uint64_t q = at(p);
+    *reinterpret_cast<uint2*>(dchunk + p) = make_uint2((uint32_t)q, (uint32_t)(q >> 32));
     p += 8;
   }
-  if (p + 4 <= hi) { *reinterpret_cast<uint32_t*>(dchunk + p) = dw(p); p += 4; }
-  if (p + 2 <= hi) { *reinterpret_cast<uint16_t*>(dchunk + p) = (uint16_t)(dw(p) >> (8 * (p & 3))); p += 2; }
-  if (p < hi) dchunk[p] = (uint8_t)(dw(p) >> (8 * (p & 3)));
+  if (p + 4 <= hi) { *reinterpret_cast<uint32_t*>(dchunk + p) = (uint32_t)at(p); p += 4; }
+  if (p + 2 <= hi) { *reinterpret_cast<uint16_t*>(dchunk + p) = (uint16_t)at(p); p += 2; }
+  if (p < hi) dchunk[p] = (uint8_t)at(p);
 }
 
 template <bool SUM>
