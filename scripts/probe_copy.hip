@@ -48,6 +48,41 @@ __global__ __launch_bounds__(256) void probe_copy(const uint8_t* __restrict__ sr
         }
       }
     }
+  } else if (MODE == 2) {
+    // dword-aligned 16-B loads (source rounded down to 4 B), byte shift by
+    // alignbyte with the next lane's first dword
+    const int s = (int)((uintptr_t)s0 & 3);
+    const uint8_t* ab = s0 - s;
+    const uint8_t* hi = s0 + seg;
+    for (int k0 = 0; k0 < nk; k0 += 16 * U) {
+      uint4 A[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint8_t* ca = ab + 16 * (k0 + r + 16 * u);
+        A[u] = ca < hi ? *reinterpret_cast<const uint4*>(ca) : make_uint4(0, 0, 0, 0);
+      }
+      uint32_t E = 0;
+      if (r == 15) {
+        const uint8_t* ce = ab + 16 * (k0 + 16 * U);
+        if (ce < hi) E = *reinterpret_cast<const uint32_t*>(ce);
+      }
+      uint32_t Rc = row_next(A[0].x);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + r + 16 * u;
+        const uint32_t Rx = u + 1 < U ? row_next(A[u + 1 < U ? u + 1 : u].x) : E;
+        const uint32_t nx = r == 15 ? Rx : Rc;
+        Rc = Rx;
+        if (k < nk) {
+          const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(A[u].y, A[u].x, s),
+                                     __builtin_amdgcn_alignbyte(A[u].z, A[u].y, s),
+                                     __builtin_amdgcn_alignbyte(A[u].w, A[u].z, s),
+                                     __builtin_amdgcn_alignbyte(nx, A[u].w, s));
+          *reinterpret_cast<uint4*>(d0 + 16 * k) = v;
+          acc += v.x ^ v.w;
+        }
+      }
+    }
   } else {
     const int s = (int)((uintptr_t)s0 & 15);
     const uint8_t* ab = s0 - s;
@@ -85,7 +120,10 @@ __global__ __launch_bounds__(256) void probe_copy(const uint8_t* __restrict__ sr
 extern "C" int probe_copy_launch(const void* src, void* dst, uint32_t nseg, uint32_t seg, uint32_t stride, int mode,
                                  void* sink, void* stream) {
   const dim3 grid((nseg + 15) / 16);
-  if (mode == 0)
+  if (mode == 2)
+    hipLaunchKernelGGL((probe_copy<6, 2>), grid, dim3(256), 0, (hipStream_t)stream, (const uint8_t*)src,
+                       (uint8_t*)dst, nseg, seg, stride, (uint32_t*)sink);
+  else if (mode == 0)
     hipLaunchKernelGGL((probe_copy<6, 0>), grid, dim3(256), 0, (hipStream_t)stream, (const uint8_t*)src,
                        (uint8_t*)dst, nseg, seg, stride, (uint32_t*)sink);
   else

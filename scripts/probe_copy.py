@@ -15,7 +15,7 @@ src = [torch.randint(0, 255, (nseg * seg + 4096,), dtype=torch.uint8, device="cu
 dst = [torch.empty(nseg * stride, dtype=torch.uint8, device="cuda") for _ in range(R)]
 sink = torch.zeros(16, dtype=torch.int32, device="cuda")
 st = torch.cuda.Stream()
-for mode in (0, 1):
+for mode in (0, 1, 2):
     for mis in (0, 1, 6):
         def go(k):
             L.probe_copy_launch(src[k % R].data_ptr() + mis, dst[k % R].data_ptr(), nseg, seg, stride, mode,
@@ -36,5 +36,5 @@ for mode in (0, 1):
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / 200
         nb = 2 * nseg * seg
-        print(json.dumps({"mode": ["unaligned", "funnel"][mode], "misalign": mis, "us": round(us, 2),
+        print(json.dumps({"mode": ["unaligned", "funnel", "dword-aligned+alignbyte"][mode], "misalign": mis, "us": round(us, 2),
                           "GBps_rw": round(nb / us / 1e3, 1), "check": ok}), flush=True)

@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
                                                              const wgcs_pkt* __restrict__ pkts,
                                                              const uint64_t* __restrict__ initial,
                                                              uint32_t n, void* __restrict__ out,
-                                                             int inplace) {
+                                                             int inplace, uint32_t amask) {
   static_assert(G == 16 || G == 64, "group = DPP row or wave");
   constexpr int PPW = 64 / G;  // packets per wave per step
   const int lane = threadIdx.x & 63;
@@ -130,7 +130,10 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
     if (r.fld + 2 > lo_all && r.fld < hi_all) hole_end = max(hole_end, r.fld + 2);
     // keep pointer provenance from the kernel argument (global address space):
     // an integer round trip would turn the loads into flat_load (full waits)
-    const int rel0 = lo_all - (int)((pbase + (uintptr_t)lo_all) & 15u);  // in [lo_all-15, lo_all]
+    // chunk grid origin: rounded down to `amask + 1` bytes (16, or a cache-line
+    // multiple so each row's loads cover whole lines); chunks wholly before
+    // lo_all are edge chunks with an empty mask and are not loaded
+    const int rel0 = lo_all - (int)((pbase + (uintptr_t)lo_all) & amask);
     const int nch = hi_all > lo_all ? (hi_all - rel0 + 15) >> 4 : 0;
     int c_lo = min((hole_end - rel0 + 15) >> 4, nch);  // first unmasked chunk
     int c_hi = max((hi_all - rel0) >> 4, c_lo);        // end of unmasked chunks
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
     uint32_t acc = 0;
     // edge chunks: issued first, consumed after the first interior batch is in flight
     int ce = sub < c_lo ? sub : c_hi + (sub - c_lo);
-    uint4 ve = sub < n_edge ? ld_chunk<NT>(src + ce) : make_uint4(0, 0, 0, 0);
+    uint4 ve = (sub < n_edge && rel0 + 16 * ce + 16 > lo_all) ? ld_chunk<NT>(src + ce) : make_uint4(0, 0, 0, 0);
     bool edge_pending = true;
     for (int c0 = c_lo + sub; c0 < c_hi || edge_pending; c0 += G * U) {
       uint4 v[U];
@@ -154,7 +157,7 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
           e += G;
           if (e >= n_edge) break;
           ce = e < c_lo ? e : c_hi + (e - c_lo);
-          ve = ld_chunk<NT>(src + ce);
+          ve = rel0 + 16 * ce + 16 > lo_all ? ld_chunk<NT>(src + ce) : make_uint4(0, 0, 0, 0);
         }
         edge_pending = false;
       }
@@ -197,14 +200,15 @@ static hipError_t launch_mode(uint8_t* arena, const wgcs_pkt* pkts, const uint64
   long want = ((long)n + ppb - 1) / ppb;
   long cap = (long)num_cu * t.blocks_per_cu;
   const int grid = (int)(want < cap ? want : cap);
+  const uint32_t amask = (uint32_t)(t.align >= 16 ? t.align : 16) - 1u;
 #define WGCS_LAUNCH(G, U)                                                                                        \
   do {                                                                                                            \
     if (t.nt)                                                                                                     \
       hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, true>), dim3(grid), dim3(256), 0, s, arena, pkts, init, \
-                         n, out, inplace);                                                                        \
+                         n, out, inplace, amask);                                                                 \
     else                                                                                                          \
       hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, false>), dim3(grid), dim3(256), 0, s, arena, pkts,    \
-                         init, n, out, inplace);                                                                  \
+                         init, n, out, inplace, amask);                                                           \
   } while (0)
   if (t.lanes_per_pkt == 64) {
     if (t.unroll >= 4) WGCS_LAUNCH(64, 4);

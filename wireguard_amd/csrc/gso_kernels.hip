@@ -30,6 +30,28 @@
 #include "wgcs_copy.h"
 #include "wgcs_kernels.h"
 
+// Timing-experiment knobs (scripts/exp_gso.sh builds variants into exp/);
+// the product library is always built with WGCS_GSO_EXP = 0.
+#ifndef WGCS_GSO_EXP
+#define WGCS_GSO_EXP 0
+#endif
+#if WGCS_GSO_EXP & 64
+__device__ unsigned long long g_gso_stamps[1 << 16];
+#define GSO_STAMP(k)                                                                                         \
+  do {                                                                                                       \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                              \
+    if ((threadIdx.x & 63) == 0)                                                                             \
+      g_gso_stamps[(((blockIdx.y * gridDim.x + blockIdx.x) * 16 + (threadIdx.x >> 6)) * 8 + (k)) & 0xFFFF] = t_; \
+  } while (0)
+extern "C" int wgcs_exp_stamps(void* host, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gso_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define GSO_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 namespace wgcs {
 
 namespace {
@@ -594,30 +616,111 @@ __device__ __forceinline__ void put_be16_u(uint4& P, int r, int pos, uint32_t va
   }
 }
 
+// Job-level values decoded once per block by wave 0 and broadcast through LDS.
+struct JobInfo {
+  int32_t status, count, nseg, type, ipv, hdr_len, gso, cs, co, plen, flags, fast;
+  uint32_t id0, seq0, ip_base, l4_base, addr, tflags;
+};
+
+__device__ __forceinline__ int ufl(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// 16 bytes at the 4-byte aligned address p (global_load_dwordx4 tolerates
+// dword alignment), optionally non-temporal.
+template <bool NT>
+__device__ __forceinline__ uint4 ld16_a4(const uint8_t* p) {
+  typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+  const u32x4a4* q = reinterpret_cast<const u32x4a4*>(__builtin_assume_aligned(p, 4));
+  const u32x4a4 t = NT ? __builtin_nontemporal_load(q) : *q;
+  return make_uint4(t.x, t.y, t.z, t.w);
+}
+
+// The dword-aligned 16-byte window at p, of which only bytes below `hi` are
+// needed: one load when the window cannot cross into a page past the last
+// needed byte, else per-dword loads (each dword holds a needed byte or is skipped).
+template <bool NT>
+__device__ __forceinline__ uint4 ld_window(const uint8_t* p, const uint8_t* hi) {
+  const uintptr_t a = (uintptr_t)p, h = (uintptr_t)hi;
+  if (a + 16 <= h || ((a + 15) >> 12) == ((h - 1) >> 12)) return ld16_a4<NT>(p);
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(p, 4));
+  uint4 v = make_uint4(0, 0, 0, 0);
+  v.x = d[0];  // p < hi: the first dword holds a needed byte
+  if (a + 4 < h) v.y = d[1];
+  if (a + 8 < h) v.z = d[2];
+  if (a + 12 < h) v.w = d[3];
+  return v;
+}
+
+// Row-per-segment split.  Block = 1024 threads = 64 rows of 16 lanes = 64
+// consecutive output segments of one job; grid = (job, segment group).
+// Wave 0 decodes the job (validation, geometry, job-constant header sums)
+// once and broadcasts it through LDS -- per-wave decoding made the CU's
+// shared scalar unit the bottleneck (16 decodes per CU).
 template <int U, bool NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gso_rows_kernel(
-    const uint8_t* __restrict__ arena, const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
-    uint8_t* __restrict__ out, uint32_t out_stride, uint32_t offset, uint32_t room, int32_t* __restrict__ sizes,
-    int32_t* __restrict__ count, int32_t* __restrict__ status) {
+__global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restrict__ arena,
+                                                        const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
+                                                        uint8_t* __restrict__ out, uint32_t out_stride,
+                                                        uint32_t offset, uint32_t room, int32_t* __restrict__ sizes,
+                                                        int32_t* __restrict__ count, int32_t* __restrict__ status) {
+  __shared__ JobInfo ji;
   const int lane = threadIdx.x & 63;
   const int r = lane & 15;
   const int wv = threadIdx.x >> 6;
   const uint32_t jb = blockIdx.x;
+  GSO_STAMP(0);
   const uint8_t* vb = arena + jobs[jb].off;
-  const uint32_t jlen = jobs[jb].len;
-  HdrBytes hb;
-  hb.load(vb, (int)min(jlen, 256u), lane);
-  const Job j = decode_job(hb, jlen, jobs[jb].flags, room, max_segs);
-  const bool ok = j.status == 0 || j.status == WGCS_ERR_TOO_MANY_SEGMENTS;
-  if (blockIdx.y == 0 && threadIdx.x == 0) {
-    count[jb] = ok ? j.count : 0;
-    status[jb] = j.status;
-  }
-  if (!ok) return;
-  const uint32_t seg0 = blockIdx.y * 16u + (uint32_t)wv * 4u;  // wave-uniform
   const uint8_t* rb = vb + 10;
   const uint64_t slot0 = (uint64_t)jb * max_segs;
-  if (j.type == GSO_NONE) {  // one packet: whole wave 0 of the job's first block
+  if (wv == 0) {
+    const uint32_t jlen = jobs[jb].len;
+    HdrBytes hb;
+    hb.load(vb, (int)min(jlen, 256u), lane);
+    const Job j = decode_job(hb, jlen, jobs[jb].flags, room, max_segs);
+    const bool ok = j.status == 0 || j.status == WGCS_ERR_TOO_MANY_SEGMENTS;
+    HdrFast hf = {};
+    uint32_t id0 = 0, seq0 = 0;
+    if (ok && j.type != GSO_NONE) {  // wave-uniform: all lanes live
+      hf = header_fast(hb, j, lane);
+      id0 = j.ipv == 4 ? hb.be16(10 + 4) : 0u;
+      seq0 = j.type != GSO_UDP_L4 ? hb.be32(10 + j.cs + 4) : 0u;
+    }
+    if (lane == 0) {
+      ji.status = j.status;
+      ji.count = ok ? j.count : 0;
+      ji.nseg = ok ? j.nseg : 0;
+      ji.type = j.type;
+      ji.ipv = j.ipv;
+      ji.hdr_len = j.hdr_len;
+      ji.gso = j.gso;
+      ji.cs = j.cs;
+      ji.co = j.co;
+      ji.plen = j.plen;
+      ji.flags = j.flags;
+      ji.fast = hf.fast ? 1 : 0;
+      ji.id0 = id0;
+      ji.seq0 = seq0;
+      ji.ip_base = hf.ip_base;
+      ji.l4_base = hf.l4_base;
+      ji.addr = hf.addr;
+      ji.tflags = hf.flags;
+      if (blockIdx.y == 0) {
+        count[jb] = ji.count;
+        status[jb] = j.status;
+      }
+    }
+  }
+  __syncthreads();
+  GSO_STAMP(1);
+  Job j = {};
+  j.status = ufl(ji.status);
+  j.nseg = ufl(ji.nseg);
+  j.type = ufl(ji.type);
+  const uint32_t seg0 = blockIdx.y * 64u + (uint32_t)wv * 4u;  // wave-uniform
+  if (j.nseg == 0) return;  // error status (or an empty packet)
+  j.plen = ufl(ji.plen);
+  j.cs = ufl(ji.cs);
+  j.co = ufl(ji.co);
+  j.flags = ufl(ji.flags);
+  if (j.type == GSO_NONE) {  // one packet: wave 0 of the job's first block
     if (seg0 == 0) {
       none_segment(rb, j, out + slot0 * out_stride + offset, lane);
       if (lane == 0) sizes[slot0] = j.plen;
@@ -625,11 +728,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     return;
   }
   if (seg0 >= (uint32_t)j.nseg) return;
-  // job-uniform header values, read across the wave while every lane is live
+  j.ipv = ufl(ji.ipv);
+  j.hdr_len = ufl(ji.hdr_len);
+  j.gso = ufl(ji.gso);
+  const bool fast = ufl(ji.fast) != 0;
+  const uint32_t id0 = (uint32_t)ufl((int)ji.id0), seq0 = (uint32_t)ufl((int)ji.seq0);
+  const uint32_t ip_base = (uint32_t)ufl((int)ji.ip_base), l4_base = (uint32_t)ufl((int)ji.l4_base);
+  const uint32_t addr_sum = (uint32_t)ufl((int)ji.addr), tflags = (uint32_t)ufl((int)ji.tflags);
   const bool v4 = j.ipv == 4, tcp = j.type != GSO_UDP_L4;
-  const uint32_t id0 = v4 ? hb.be16(10 + 4) : 0u;
-  const uint32_t seq0 = tcp ? hb.be32(10 + j.cs + 4) : 0u;
-  const HdrFast hf = header_fast(hb, j, lane);
   const int i = (int)seg0 + (lane >> 4);
   if (i >= j.nseg) return;  // whole rows retire; DPP below stays inside live rows
 
@@ -648,8 +754,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   const int nk = (pkt_len + dalign + 15) >> 4;
   const int hk = min((hdr_len + dalign + 15) >> 4, nk);
   const uint8_t* w0 = rb + i * j.gso - dalign;  // source of destination chunk 0 (payload positions)
-  const int s = (int)((uintptr_t)w0 & 15u);
-  const uint8_t* abase = w0 - s;
+  const int sb = (int)((uintptr_t)w0 & 3u);     // byte shift within dwords
+  const uint8_t* abase = w0 - sb;               // dword-aligned window base
   const uint8_t* src_lo = rb + seg_start;
   const uint8_t* src_hi = rb + seg_end;
   const uint4 z = make_uint4(0, 0, 0, 0);
@@ -658,15 +764,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   // fast: packet coordinates (lane r = readBuf[16r, 16r + 16), wave-uniform
   // phase); general: destination coordinates (per-row phase).
   const uint8_t* hend = rb + hdr_len;
-  const int hph = hf.fast ? (int)((uintptr_t)rb & 15u) : (int)((uintptr_t)(rb - dalign) & 15u);
-  const uint8_t* hab = (hf.fast ? rb : rb - dalign) - hph + 16 * r;
+  const int hph = fast ? (int)((uintptr_t)rb & 15u) : (int)((uintptr_t)(rb - dalign) & 15u);
+  const uint8_t* hab = (fast ? rb : rb - dalign) - hph + 16 * r;
   uint4 H0 = z, H1 = z;
   if (r < hk) {
     if (hab < hend && hab + 16 > rb) H0 = ld16(hab);
     if (hab + 16 < hend && hab + 32 > rb) H1 = ld16(hab + 16);
   }
 
-  // ---- payload stream
+  // ---- payload stream: destination chunk k = bytes [sb, sb + 16) of the
+  // dword-aligned window k and the first dword of window k + 1 (next lane, DPP)
   uint32_t acc = 0;  // L4 bytes [hdrLen, pktLen): LE words at destination addresses
   uint4 keep = z;    // payload part of header chunk r (r < hk)
   for (int k0 = 0; k0 < nk; k0 += 16 * U) {
@@ -674,22 +781,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint8_t* ca = abase + 16 * (k0 + r + 16 * u);
-      A[u] = (ca < src_hi && ca + 16 > src_lo) ? ld_src<NT>(ca) : z;
+      A[u] = (ca < src_hi && ca + 16 > src_lo) ? ld_window<NT>(ca, src_hi) : z;
     }
-    uint4 E = z;
+    uint32_t E = 0;
     if (r == 15) {
       const uint8_t* ce = abase + 16 * (k0 + 16 * U);
-      if (ce < src_hi && ce + 16 > src_lo) E = ld_src<NT>(ce);
+      if (ce < src_hi && ce + 4 > src_lo) E = *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(ce, 4));
     }
-    uint4 Rc = row_next4(A[0]);  // chunk k + 1 comes from the next lane (lane 15: lane 0's next u)
+    uint32_t Rc = row_next(A[0].x);  // lane 15: lane 0's next-u dword
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = k0 + r + 16 * u;
-      const uint4 Rx = u + 1 < U ? row_next4(A[u + 1 < U ? u + 1 : u]) : E;
-      const uint4 B = r == 15 ? Rx : Rc;
+      const uint32_t Rx = u + 1 < U ? row_next(A[u + 1 < U ? u + 1 : u].x) : E;
+      const uint32_t nx = r == 15 ? Rx : Rc;
       Rc = Rx;
       if (k < nk) {
-        const uint4 v = funnel_v(A[u], B, s);
+        const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(A[u].y, A[u].x, sb),
+                                   __builtin_amdgcn_alignbyte(A[u].z, A[u].y, sb),
+                                   __builtin_amdgcn_alignbyte(A[u].w, A[u].z, sb),
+                                   __builtin_amdgcn_alignbyte(nx, A[u].w, sb));
         const int x0 = 16 * k - dalign;
         if (x0 >= hdr_len && x0 + 16 <= pkt_len) acc = add4(acc, v);
         else acc = add4_masked(acc, v, byte_bits16(hdr_len - x0, pkt_len - x0), false);
@@ -698,6 +808,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
       }
     }
   }
+  GSO_STAMP(3);
 
   const uint32_t id = i > 0 ? ((id0 + 1) & 0xFFFFu) : id0;  // quirk: id0 + 1 for every i >= 1 (:1426-1431)
   const uint32_t seq = seq0 + (uint32_t)(uint16_t)((uint16_t)j.gso * (uint16_t)i);  // uint16 product (:1445)
@@ -707,16 +818,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   const int x0h = 16 * r - dalign;
   const uint32_t hmask = byte_bits16(-x0h, hdr_len - x0h);  // header positions of destination chunk r
 
-  if (hf.fast) {
+  if (fast) {
     // ---- sums: payload (row reduction) + job constants + rewritten fields
     uint32_t t_pay = fold32_16(row16_sum_u32(acc));
     if ((((uintptr_t)dst + (uintptr_t)cs) & 1u) == 0) t_pay = bswap16(t_pay);  // pairing from csumStart
-    const uint32_t var = tcp ? (seq >> 16) + (seq & 0xFFFFu) + (last ? (hf.flags & 0x09u) : 0u) : ulen;
-    const uint32_t l4c = (~fold32_16(t_pay + fold32_16(hf.l4_base) + var + fold32_16(hf.addr) + proto + tlen)) & 0xFFFFu;
+    const uint32_t var = tcp ? (seq >> 16) + (seq & 0xFFFFu) + (last ? (tflags & 0x09u) : 0u) : ulen;
+    const uint32_t l4c = (~fold32_16(t_pay + fold32_16(l4_base) + var + fold32_16(addr_sum) + proto + tlen)) & 0xFFFFu;
     // ---- header chunk in packet coordinates, rewritten (gro.go:1418-1465, :1486-1490)
     uint4 P = funnel(H0, H1, hph);
     if (v4) {
-      const uint32_t ipc = (~fold32_16(fold32_16(hf.ip_base) + (uint32_t)pkt_len + id)) & 0xFFFFu;
+      const uint32_t ipc = (~fold32_16(fold32_16(ip_base) + (uint32_t)pkt_len + id)) & 0xFFFFu;
       put_be16_u(P, r, 2, (uint32_t)pkt_len);  // total length (:1433)
       put_be16_u(P, r, 4, id);                 // identification (:1426-1431)
       put_be16_u(P, r, 10, ipc);               // header checksum (:1434-1436)
@@ -726,7 +837,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     if (tcp) {
       put_be16_u(P, r, cs + 4, seq >> 16);  // sequence number (:1445-1446)
       put_be16_u(P, r, cs + 6, seq);
-      put_u(P, r, cs + 13, last ? hf.flags : (hf.flags & ~0x09u), 0xFFu);  // FIN|PSH on the last only (:1447-1459)
+      put_u(P, r, cs + 13, last ? tflags : (tflags & ~0x09u), 0xFFu);  // FIN|PSH on the last only (:1447-1459)
     } else {
       put_be16_u(P, r, cs + 4, ulen);
     }
@@ -776,6 +887,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     }
   }
   if (r == 0) sizes[slot] = pkt_len;
+  GSO_STAMP(4);
 }
 
 static int gso_impl() {
@@ -796,9 +908,9 @@ hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs
   if (n_jobs == 0 || max_segs == 0) return hipSuccess;
   const uint32_t room = out_stride > offset ? out_stride - offset : 0;
   if (gso_impl() == 0) {
-    const uint32_t gy = (max_segs + 15) / 16;
+    const uint32_t gy = (max_segs + 63) / 64;
     if (gy > 65535u) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((gso_rows_kernel<6, true>), dim3(n_jobs, gy), dim3(256), 0, s, arena, jobs, max_segs, out,
+    hipLaunchKernelGGL((gso_rows_kernel<6, true>), dim3(n_jobs, gy), dim3(1024), 0, s, arena, jobs, max_segs, out,
                        out_stride, offset, room, sizes, count, status);
     return hipGetLastError();
   }

@@ -13,6 +13,7 @@ struct LaunchTuning {
   int lanes_per_pkt = 16;  // 16: one DPP row per packet (4 per wave); 64: one wave per packet
   int unroll = 6;          // 16-byte loads in flight per lane per iteration
   int nt = 1;              // non-temporal (streaming) loads: each byte is read once
+  int align = 16;          // chunk grid origin: packet start rounded down to this many bytes
 };
 
 hipError_t launch_checksum_batch(int mode, unsigned flags, uint8_t* arena, const wgcs_pkt* pkts,
