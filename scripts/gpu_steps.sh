@@ -25,7 +25,6 @@ for s in "$@"; do
     tests) step tests 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     tests-all) step tests 1100 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     tests-gso) step tests_gso 600 python -m pytest tests/test_gpu_gso.py tests/test_golden.py -m gpu -q -p no:cacheprovider ;;
-    bench-cfg4-legacy) step bench_cfg4_legacy 300 env WGCS_GSO_IMPL=1 python bench.py --config cfg4 --steps 100 --warmup 10 --cpu-seconds 0 ;;
     sweep) step sweep 400 python scripts/sweep_checksum.py ;;
     sweep-align) step sweep_align 400 python scripts/sweep_checksum.py --variants 16:6:8:1:16,16:6:8:1:64,16:6:8:1:128,16:8:8:1:16,16:8:8:1:64,16:8:8:1:128 ;;
     sweep-cfg3) step sweep_cfg3 400 python scripts/sweep_checksum.py --config cfg3 ;;

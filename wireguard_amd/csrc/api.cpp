@@ -113,7 +113,7 @@ int wgcs_destroy(wgcs_ctx* ctx) {
   if (!ctx) return WGCS_ERR_INVALID_ARG;
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
-  for (DevBuf* b : {&ctx->d_arena, &ctx->d_pkts, &ctx->d_init, &ctx->d_out, &ctx->d_out2, &ctx->d_aux, &ctx->d_ws})
+  for (DevBuf* b : {&ctx->d_arena, &ctx->d_pkts, &ctx->d_init, &ctx->d_out, &ctx->d_out2, &ctx->d_aux})
     if (b->ptr) hipFree(b->ptr);
   for (HostBuf* b : {&ctx->h_stage, &ctx->h_meta, &ctx->h_out})
     if (b->ptr) hipHostFree(b->ptr);

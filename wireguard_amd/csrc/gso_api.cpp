@@ -56,10 +56,9 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->d_aux.ptr, hjob, sizeof(wgcs_gso_job), hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemsetAsync(d_sizes, 0, meta, s);
   if (e != hipSuccess) return hip_fail(ctx, e, "H2D");
-  if (gso_workspace_bytes(1) && (rc = ensure_dev(ctx, ctx->d_ws, gso_workspace_bytes(1)))) return rc;
   e = launch_gso_split_batch((const uint8_t*)ctx->d_arena.ptr, (const wgcs_gso_job*)ctx->d_aux.ptr, 1,
                              (uint8_t*)ctx->d_out.ptr, (uint32_t)stride, (uint32_t)offset, (uint32_t)nbufs, d_sizes,
-                             d_count, d_status, ctx->d_ws.ptr, s, ctx->num_cu);
+                             d_count, d_status, s);
   if (e != hipSuccess) return hip_fail(ctx, e, "gso_split launch");
   int32_t* h = (int32_t*)ctx->h_meta.ptr;
   e = hipMemcpyAsync(h, d_sizes, meta, hipMemcpyDeviceToHost, s);
@@ -108,12 +107,8 @@ int wgcs_gso_split_batch(wgcs_ctx* ctx, const uint8_t* d_arena, const wgcs_gso_j
   hipSetDevice(ctx->device);
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   if ((uint64_t)n_jobs * max_segs > 0xFFFFFFFFull) return set_err(ctx, WGCS_ERR_INVALID_ARG, "n_jobs*max_segs >= 2^32");
-  // per-job plans live in a context workspace (grown here, never inside a capture)
-  const size_t ws = gso_workspace_bytes(n_jobs);
-  int rc = ws ? ensure_dev(ctx, ctx->d_ws, ws) : WGCS_OK;
-  if (rc) return rc;
   hipError_t e = launch_gso_split_batch(d_arena, d_jobs, n_jobs, d_out, out_stride, offset, max_segs, d_sizes, d_count,
-                                        d_status, ctx->d_ws.ptr, s, ctx->num_cu);
+                                        d_status, s);
   return e == hipSuccess ? WGCS_OK : hip_fail(ctx, e, "gso_split_batch launch");
 }
 

@@ -152,56 +152,6 @@ __device__ __forceinline__ void stream_copy(const uint8_t* src0, const uint8_t* 
   }
 }
 
-// First 128 destination chunks of a stream_copy, split into an early load
-// phase (issue the HBM loads, keep them in flight) and a later store phase,
-// so independent work (GSO header assembly) hides the load latency.
-struct CopyBatch {
-  uint4 a0, a1, e0, e1;  // own chunks and lane 63's next chunks
-  const uint8_t* abase;
-  int s, k0;
-};
-
-__device__ __forceinline__ CopyBatch copy_batch_load(const uint8_t* src0, const uint8_t* src_lo, const uint8_t* src_hi,
-                                                     int dalign, int k_begin, int k_end, int lane) {
-  CopyBatch B;
-  const uint8_t* w0 = src0 - dalign;
-  B.s = (int)((uintptr_t)w0 & 15);
-  B.abase = w0 - B.s;
-  B.k0 = k_begin;
-  const uint8_t* ca = B.abase + 16 * (long)(k_begin + lane);
-  const uint8_t* cb = ca + 64 * 16;
-  B.a0 = B.a1 = B.e0 = B.e1 = make_uint4(0, 0, 0, 0);
-  if (k_begin < k_end && ca < src_hi && ca + 16 > src_lo) B.a0 = ld16(ca);
-  if (k_begin + 64 < k_end && cb < src_hi && cb + 16 > src_lo) B.a1 = ld16(cb);
-  if (lane == 63) {
-    if (ca + 16 < src_hi && ca + 32 > src_lo) B.e0 = ld16(ca + 16);
-    if (k_begin + 64 < k_end && cb + 16 < src_hi && cb + 32 > src_lo) B.e1 = ld16(cb + 16);
-  }
-  return B;
-}
-
-template <bool SUM>
-__device__ __forceinline__ void copy_batch_store(const CopyBatch& B, uint8_t* dbase, int dalign, int k_end, int pkt_len,
-                                                 int sum_lo, int lane, uint64_t& acc) {
-  if (B.k0 >= k_end) return;
-  uint4 b0;
-  b0.x = __shfl_down(B.a0.x, 1);
-  b0.y = __shfl_down(B.a0.y, 1);
-  b0.z = __shfl_down(B.a0.z, 1);
-  b0.w = __shfl_down(B.a0.w, 1);
-  if (lane == 63) b0 = B.e0;
-  copy_tail<SUM>(B.a0, b0, B.s, B.k0 + lane, k_end, dalign, pkt_len, sum_lo, -1, 0, dbase, acc);
-  if (B.k0 + 64 < k_end) {  // wave-uniform
-    uint4 b1;
-    b1.x = __shfl_down(B.a1.x, 1);
-    b1.y = __shfl_down(B.a1.y, 1);
-    b1.z = __shfl_down(B.a1.z, 1);
-    b1.w = __shfl_down(B.a1.w, 1);
-    if (lane == 63) b1 = B.e1;
-    copy_tail<SUM>(B.a1, b1, B.s, B.k0 + 64 + lane, k_end, dalign, pkt_len, sum_lo, -1, 0, dbase, acc);
-  }
-}
-
 // dst[0:n) = src[0:n), any alignments (no checksum).
 __device__ __forceinline__ void copy_range(const uint8_t* src, int n, uint8_t* dst, int lane) {
   if (n <= 0) return;

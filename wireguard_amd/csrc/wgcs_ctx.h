@@ -35,7 +35,7 @@ struct wgcs_ctx {
   std::string last_error;
   wgcs::LaunchTuning tune;
   // device staging (grown on demand, never shrunk)
-  wgcs::DevBuf d_arena, d_pkts, d_init, d_out, d_out2, d_aux, d_ws;
+  wgcs::DevBuf d_arena, d_pkts, d_init, d_out, d_out2, d_aux;
   // pinned host staging
   wgcs::HostBuf h_stage, h_meta, h_out;
 };

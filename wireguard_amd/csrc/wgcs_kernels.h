@@ -20,12 +20,10 @@ hipError_t launch_checksum_batch(int mode, unsigned flags, uint8_t* arena, const
                                  const uint64_t* init, uint32_t n, void* out, hipStream_t s, int num_cu,
                                  const LaunchTuning& tune);
 
-// workspace: gso_workspace_bytes(n_jobs) bytes of device memory (per-job plans)
-size_t gso_workspace_bytes(uint32_t n_jobs);
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs,
                                   uint8_t* out, uint32_t out_stride, uint32_t offset, uint32_t max_segs,
-                                  int32_t* sizes, int32_t* count, int32_t* status, void* workspace,
-                                  hipStream_t s, int num_cu);
+                                  int32_t* sizes, int32_t* count, int32_t* status,
+                                  hipStream_t s);
 
 // One coalesced GRO output (applyTCPCoalesce / applyUDPCoalesce item).
 struct GroItem {
