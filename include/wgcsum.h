@@ -51,6 +51,8 @@ extern "C" {
 #define WGCS_ERR_CSUM_OFFSET (-11)      /* "end of checksum offset (%d) exceeds packet length (%d)" tun.go:625 */
 #define WGCS_ERR_READ_OVERFLOW (-12)    /* "read length %d overflows bufs element length %d" tun.go:546 */
 #define WGCS_ERR_OUT_OF_RANGE (-13)     /* input on which the Go code would panic (slice bounds) */
+#define WGCS_ERR_BATCH_FULL (-14)       /* stager: the open batch has no room; submit it first */
+#define WGCS_ERR_NOT_READY (-15)        /* stager: batch id not submitted / recycled */
 #define WGCS_ERR_HIP (-100)             /* HIP runtime error (message: wgcs_last_error) */
 #define WGCS_ERR_NOMEM (-101)
 #define WGCS_ERR_NO_DEVICE (-102)
@@ -157,6 +159,46 @@ int wgcs_handle_virtio_read(wgcs_ctx *ctx, uint8_t *read_buf, size_t n, uint8_t 
  * entries, gro.go:696-697); to_write receives the indices to write. */
 int wgcs_handle_gro(wgcs_ctx *ctx, uint8_t **bufs, size_t *lens, size_t *caps, int n,
                     int offset, int can_udp_gro, int *to_write, int *n_to_write);
+
+/* ---- Tun.Read batch staging (tun/tun.go:477-508) ----
+ * A ring of `depth` batches.  Each batch stages up to max_reads TUN reads
+ * (virtio header + packet, as read(2) returns them into tun.readBuf) in pinned
+ * host memory; wgcs_stager_submit queues H2D -> GSO split (the kernel of
+ * wgcs_gso_split_batch, handleVirtioRead semantics) -> D2H of sizes, counts,
+ * statuses and the output slots on the batch's own stream, so consecutive
+ * batches overlap both copy directions with compute.  Segment s of read r
+ * lands in pinned memory at segs + s*seg_stride (seg_stride >= the largest
+ * segment, e.g. 65535 for 64 KiB GSO_NONE reads, 1536 for MSS 1460).
+ * Only the stager's own copy of each read is used (tun.readBuf is free again
+ * as soon as push/commit returns); the reference's in-place readBuf edits are
+ * not replayed there (they are invisible to Read's callers).
+ * Ring discipline (depth >= 2): one slot is always open for pushes, so the results of a
+ * batch stay readable until depth-1 further batches have been submitted
+ * (the submit after that recycles its slot, waiting for it if still running). */
+typedef struct wgcs_stager wgcs_stager;
+int wgcs_stager_create(wgcs_ctx *ctx, uint32_t depth, uint32_t max_reads, size_t max_bytes,
+                       uint32_t max_segs, uint32_t seg_stride, wgcs_stager **out);
+int wgcs_stager_destroy(wgcs_stager *st);
+/* copy one read into the open batch (waits for the ring slot if it is still in flight) */
+int wgcs_stager_push(wgcs_stager *st, const uint8_t *read_buf, size_t n, int *read_idx);
+/* push `count` reads in one call (read_idx of the first one in *first_idx); on
+ * WGCS_ERR_BATCH_FULL *pushed tells how many went in */
+int wgcs_stager_push_many(wgcs_stager *st, const uint8_t *const *read_bufs, const size_t *ns, int count,
+                          int *first_idx, int *pushed);
+/* zero-copy form: reserve room for up to max_n bytes (read(2) goes straight
+ * into *dst), then commit the byte count read (0 drops the reservation) */
+int wgcs_stager_reserve(wgcs_stager *st, size_t max_n, uint8_t **dst, int *read_idx);
+int wgcs_stager_commit(wgcs_stager *st, int read_idx, size_t n);
+/* queue the open batch (no-op id for an empty batch) and open the next one */
+int wgcs_stager_submit(wgcs_stager *st, uint64_t *batch);
+int wgcs_stager_wait(wgcs_stager *st, uint64_t batch);
+/* results of read r of a completed batch, handleVirtioRead's (n, err) */
+int wgcs_stager_result(wgcs_stager *st, uint64_t batch, int read_idx, int *status, int *n,
+                       const int32_t **sizes, const uint8_t **segs);
+/* copy read r's segments into bufs[i][offset:] exactly as handleVirtioRead
+ * leaves them (sizes[], n, ErrTooManySegments / slice-bound checks) */
+int wgcs_stager_copy_out(wgcs_stager *st, uint64_t batch, int read_idx, uint8_t *const *bufs,
+                         const size_t *buf_lens, int nbufs, int *sizes, int offset, int *n_out);
 
 #ifdef __cplusplus
 }

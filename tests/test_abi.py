@@ -67,7 +67,7 @@ def test_python_constants_match_header():
 def test_version_and_errors():
     L = wireguard_amd.load()
     assert L.wgcs_abi_version() == _defines()["WGCS_ABI_VERSION"]
-    for code in [0, -1, -2, -3, -4, -5, -6, -7, -8, -9, -10, -11, -12, -13, -100, -101, -102]:
+    for code in [0, -1, -2, -3, -4, -5, -6, -7, -8, -9, -10, -11, -12, -13, -14, -15, -100, -101, -102]:
         assert L.wgcs_strerror(code) and L.wgcs_strerror(code) != b"unknown status"
     assert L.wgcs_strerror(-9999) == b"unknown status"
 

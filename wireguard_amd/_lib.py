@@ -29,6 +29,8 @@ ERR_HDR_LEN = -10
 ERR_CSUM_OFFSET = -11
 ERR_READ_OVERFLOW = -12
 ERR_OUT_OF_RANGE = -13
+ERR_BATCH_FULL = -14
+ERR_NOT_READY = -15
 ERR_HIP = -100
 ERR_NOMEM = -101
 ERR_NO_DEVICE = -102
@@ -95,6 +97,16 @@ def load() -> C.CDLL:
         "wgcs_handle_virtio_read": ([vp, vp, sz, u8pp, C.POINTER(sz), i32, C.POINTER(i32), i32, C.POINTER(i32)], i32),
         "wgcs_handle_gro": ([vp, u8pp, C.POINTER(sz), C.POINTER(sz), i32, i32, i32, C.POINTER(i32), C.POINTER(i32)],
                             i32),
+        "wgcs_stager_create": ([vp, u32, u32, sz, u32, u32, C.POINTER(vp)], i32),
+        "wgcs_stager_destroy": ([vp], i32),
+        "wgcs_stager_push": ([vp, vp, sz, C.POINTER(i32)], i32),
+        "wgcs_stager_push_many": ([vp, C.POINTER(vp), C.POINTER(sz), i32, C.POINTER(i32), C.POINTER(i32)], i32),
+        "wgcs_stager_reserve": ([vp, sz, C.POINTER(vp), C.POINTER(i32)], i32),
+        "wgcs_stager_commit": ([vp, i32, sz], i32),
+        "wgcs_stager_submit": ([vp, C.POINTER(u64)], i32),
+        "wgcs_stager_wait": ([vp, u64], i32),
+        "wgcs_stager_result": ([vp, u64, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(vp), C.POINTER(vp)], i32),
+        "wgcs_stager_copy_out": ([vp, u64, i32, u8pp, C.POINTER(sz), i32, C.POINTER(i32), i32, C.POINTER(i32)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -138,6 +138,8 @@ const char* wgcs_strerror(int status) {
     case WGCS_ERR_CSUM_OFFSET: return "end of checksum offset exceeds packet length";
     case WGCS_ERR_READ_OVERFLOW: return "read length overflows bufs element length";
     case WGCS_ERR_OUT_OF_RANGE: return "slice bounds out of range";
+    case WGCS_ERR_BATCH_FULL: return "staging batch full";
+    case WGCS_ERR_NOT_READY: return "batch not submitted or already recycled";
     case WGCS_ERR_HIP: return "HIP runtime error";
     case WGCS_ERR_NOMEM: return "out of memory";
     case WGCS_ERR_NO_DEVICE: return "no HIP device";

@@ -436,6 +436,7 @@ template <int U, bool NT>
 __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restrict__ arena,
                                                         const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
                                                         uint8_t* __restrict__ out, uint32_t out_stride,
+                                                        const GsoOutPos* __restrict__ outpos,
                                                         uint32_t offset, uint32_t room, int32_t* __restrict__ sizes,
                                                         int32_t* __restrict__ count, int32_t* __restrict__ status) {
   __shared__ JobInfo ji;
@@ -446,7 +447,15 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   GSO_STAMP(0);
   const uint8_t* vb = arena + jobs[jb].off;
   const uint8_t* rb = vb + 10;
-  const uint64_t slot0 = (uint64_t)jb * max_segs;
+  const uint64_t slot0 = (uint64_t)jb * max_segs;  // sizes[] index of segment 0
+  // segment i of this job at out + obase + i * opitch (+ offset): fixed slots,
+  // or the caller's packed per-job layout (the stager's compact D2H region)
+  uint64_t obase = slot0 * out_stride;
+  uint32_t opitch = out_stride;
+  if (outpos) {
+    obase = outpos[jb].base;
+    opitch = outpos[jb].pitch;
+  }
   if (wv == 0) {
     const uint32_t jlen = jobs[jb].len;
     HdrBytes hb;
@@ -499,7 +508,7 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   j.flags = ufl(ji.flags);
   if (j.type == GSO_NONE) {  // one packet: wave 0 of the job's first block
     if (seg0 == 0) {
-      none_segment(rb, j, out + slot0 * out_stride + offset, lane);
+      none_segment(rb, j, out + obase + offset, lane);
       if (lane == 0) sizes[slot0] = j.plen;
     }
     return;
@@ -525,7 +534,7 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   const int pkt_len = hdr_len + seg_len;
   const bool last = seg_end == plen;
   const uint64_t slot = slot0 + (uint32_t)i;
-  uint8_t* dst = out + slot * out_stride + offset;
+  uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
   const int dalign = (int)((uintptr_t)dst & 15u);
   uint8_t* dbase = dst - dalign;
   const int nk = (pkt_len + dalign + 15) >> 4;
@@ -669,13 +678,14 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
 
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs, uint8_t* out,
                                   uint32_t out_stride, uint32_t offset, uint32_t max_segs, int32_t* sizes,
-                                  int32_t* count, int32_t* status, hipStream_t s) {
+                                  int32_t* count, int32_t* status, hipStream_t s, const GsoOutPos* outpos,
+                                  uint32_t room) {
   if (n_jobs == 0 || max_segs == 0) return hipSuccess;
-  const uint32_t room = out_stride > offset ? out_stride - offset : 0;
+  if (!outpos) room = out_stride > offset ? out_stride - offset : 0;
   const uint32_t gy = (max_segs + 63) / 64;  // 64 segments (rows) per 1024-thread block
   if (gy > 65535u) return hipErrorInvalidValue;
   hipLaunchKernelGGL((gso_rows_kernel<6, true>), dim3(n_jobs, gy), dim3(1024), 0, s, arena, jobs, max_segs, out,
-                     out_stride, offset, room, sizes, count, status);
+                     out_stride, outpos, offset, room, sizes, count, status);
   return hipGetLastError();
 }
 

@@ -20,10 +20,19 @@ hipError_t launch_checksum_batch(int mode, unsigned flags, uint8_t* arena, const
                                  const uint64_t* init, uint32_t n, void* out, hipStream_t s, int num_cu,
                                  const LaunchTuning& tune);
 
+// Optional packed output layout: segment i of job j at out + base + i*pitch
+// (+ offset); pitch must hold the job's largest segment.  The room checks
+// (handleVirtioRead's bufs element length) then use `room` instead of
+// out_stride - offset.
+struct GsoOutPos {
+  uint64_t base;
+  uint32_t pitch;
+  uint32_t pad;
+};
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs,
                                   uint8_t* out, uint32_t out_stride, uint32_t offset, uint32_t max_segs,
                                   int32_t* sizes, int32_t* count, int32_t* status,
-                                  hipStream_t s);
+                                  hipStream_t s, const GsoOutPos* outpos = nullptr, uint32_t room = 0);
 
 // One coalesced GRO output (applyTCPCoalesce / applyUDPCoalesce item).
 struct GroItem {

@@ -118,6 +118,8 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
             "d2d_copy_same_bytes_ms": round(copy_ms, 5),
         },
     }
+    if not getattr(args, "no_e2e", False):
+        result["end_to_end"] = end_to_end(dev, pkts, bytes_in, bytes_out, steps=max(10, min(args.steps, 40)))
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(pkts, args.cpu_seconds, bytes_per_step)
     if rank == 0:
@@ -125,6 +127,42 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
     dev.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def end_to_end(dev, pkts, bytes_in, bytes_out, steps: int, depth: int = 3):
+    """Host-memory-in / host-memory-out rate through the Tun.Read stager
+    (wgcs_stager_*): per batch, the 256 reads are copied into the pinned ring
+    slot (standing in for read(2) into tun.readBuf), then H2D -> split -> D2H
+    of the packed segments on the slot's stream; `depth` batches in flight."""
+    from .tun import Stager
+
+    arrs = [np.frombuffer(p, np.uint8) for p in pkts]
+    st = Stager(dev, depth=depth, max_reads=len(arrs), max_bytes=sum(len(a) + 16 for a in arrs), max_segs=64,
+                seg_room=1536 - 16)
+    inflight = []
+
+    def one():
+        st.push_many(arrs)
+        if len(inflight) == depth - 1:  # the next submit recycles the oldest slot: consume it first
+            b = inflight.pop(0)
+            st.wait(b)
+            n, err, _ = st.result(b, len(arrs) - 1)
+            assert err is None and n == 45
+        inflight.append(st.submit())
+
+    for _ in range(depth + 2):
+        one()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    while inflight:
+        st.wait(inflight.pop(0))
+    dt = (time.perf_counter() - t0) / steps
+    st.close()
+    return {"value": round((bytes_in + bytes_out) / dt / 2**30, 2), "unit": "GiB/s",
+            "ms_per_batch": round(dt * 1e3, 4), "bytes_in_plus_out": bytes_in + bytes_out,
+            "what": f"Tun.Read stager, depth {depth}: host memcpy of the reads into pinned staging + H2D + "
+                    "split kernel + D2H of the packed segments (PCIe-inclusive)"}
 
 
 def cpu_baseline(pkts, seconds, bytes_per_step):

@@ -37,7 +37,7 @@ VIRTIO_NET_HDR_GSO_TCPV6 = 4
 VIRTIO_NET_HDR_GSO_UDP_L4 = 5
 
 __all__ = [
-    "Device", "PKT_DTYPE", "GSO_JOB_DTYPE", "MODE_FOLD", "MODE_L4_FILL", "MODE_VALIDATE", "MODE_PARTIAL",
+    "Device", "Stager", "PKT_DTYPE", "GSO_JOB_DTYPE", "MODE_FOLD", "MODE_L4_FILL", "MODE_VALIDATE", "MODE_PARTIAL",
     "MODE_IP4HDR", "F_INPLACE", "PKT_V6", "PKT_UDP", "VirtioHdr", "WgcsError",
 ]
 
@@ -201,3 +201,86 @@ class Device:
         rc = self.lib.wgcs_handle_gro(self.h, arr, clens, ccaps, n, offset, int(can_udp_gro), tw, C.byref(ntw))
         order = [orig.index(C.cast(arr[i], C.c_void_p).value) for i in range(n)]
         return list(tw)[: ntw.value], order, list(clens), self._err(rc)
+
+
+class Stager:
+    """Tun.Read batch staging ring (include/wgcsum.h wgcs_stager_*): many TUN
+    reads -> one GSO-split launch with pipelined H2D / kernel / D2H.
+
+    Create it with max_segs = len(bufs) and seg_room = len(bufs[i]) - offset of
+    the Read caller's buffers; then copy_out() leaves bufs/sizes exactly as
+    handleVirtioRead (tun/tun.go:514-632) would for that read.  Results of a
+    batch stay readable until depth-1 more batches have been submitted."""
+
+    def __init__(self, dev: Device, depth: int, max_reads: int, max_bytes: int, max_segs: int, seg_room: int):
+        self.dev, self.lib = dev, dev.lib
+        h = C.c_void_p()
+        dev._check(self.lib.wgcs_stager_create(dev.h, depth, max_reads, max_bytes, max_segs, seg_room, C.byref(h)))
+        self.h = h
+        self.max_segs = max_segs
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.wgcs_stager_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def push(self, read_buf) -> int:
+        a = _np_u8(read_buf)
+        idx = C.c_int(0)
+        self.dev._check(self.lib.wgcs_stager_push(self.h, _ptr(a), len(a), C.byref(idx)))
+        return idx.value
+
+    def push_many(self, reads: list) -> int:
+        """Push several reads with one call; returns the first read index."""
+        arrs = [_np_u8(r) for r in reads]
+        ptrs = (C.c_void_p * len(arrs))(*[a.ctypes.data if len(a) else None for a in arrs])
+        ns = (C.c_size_t * len(arrs))(*[len(a) for a in arrs])
+        first, pushed = C.c_int(0), C.c_int(0)
+        self.dev._check(self.lib.wgcs_stager_push_many(self.h, ptrs, ns, len(arrs), C.byref(first), C.byref(pushed)))
+        return first.value
+
+    def reserve(self, max_n: int):
+        """(read_idx, writable uint8 view of the pinned staging) for a read(2)."""
+        p, idx = C.c_void_p(), C.c_int(0)
+        self.dev._check(self.lib.wgcs_stager_reserve(self.h, max_n, C.byref(p), C.byref(idx)))
+        view = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(max_n,)) if max_n else \
+            np.zeros(0, np.uint8)
+        return idx.value, view
+
+    def commit(self, read_idx: int, n: int) -> None:
+        self.dev._check(self.lib.wgcs_stager_commit(self.h, read_idx, n))
+
+    def submit(self) -> int:
+        b = C.c_uint64(0)
+        self.dev._check(self.lib.wgcs_stager_submit(self.h, C.byref(b)))
+        return b.value
+
+    def wait(self, batch: int) -> None:
+        self.dev._check(self.lib.wgcs_stager_wait(self.h, batch))
+
+    def result(self, batch: int, read_idx: int):
+        """(n, err, sizes) of one read, handleVirtioRead's return values."""
+        st, n = C.c_int(0), C.c_int(0)
+        sz = C.c_void_p()
+        self.dev._check(self.lib.wgcs_stager_result(self.h, batch, read_idx, C.byref(st), C.byref(n), C.byref(sz),
+                                                    None))
+        k = self.max_segs if st.value == _lib.ERR_TOO_MANY_SEGMENTS else max(n.value, 0)
+        sizes = list(np.ctypeslib.as_array(C.cast(sz, C.POINTER(C.c_int32)), shape=(self.max_segs,))[:k])
+        return n.value, self.dev._err(st.value), sizes
+
+    def copy_out(self, batch: int, read_idx: int, bufs: list, sizes: list, offset: int):
+        """Scatter one read's segments into bufs[i][offset:]; returns (n, err)."""
+        arr, lens = Device._bufs(bufs)
+        csz = (C.c_int * len(bufs))()
+        n = C.c_int(0)
+        rc = self.lib.wgcs_stager_copy_out(self.h, batch, read_idx, arr, lens, len(bufs), csz, offset, C.byref(n))
+        if rc in (_lib.ERR_INVALID_ARG, _lib.ERR_NOT_READY, _lib.ERR_HIP):
+            self.dev._check(rc)
+        sizes[: len(bufs)] = list(csz)
+        return n.value, self.dev._err(rc)
