@@ -141,13 +141,14 @@ def handle_gro(bufs: list, lens: list, offset: int, can_udp_gro: bool):
     n = len(bufs)
     u8p = C.POINTER(C.c_uint8)
     arr = _bufs_ctypes(bufs)
-    orig = [C.cast(arr[i], C.c_void_p).value for i in range(n)]
+    orig = {b.ctypes.data: i for i, b in enumerate(bufs)}
     clens = (C.c_size_t * n)(*lens)
     ccaps = (C.c_size_t * n)(*[len(b) for b in bufs])
     tw = (C.c_int * n)()
     ntw = C.c_int(0)
     rc = lib().or_handle_gro(arr, clens, ccaps, n, offset, int(can_udp_gro), tw, C.byref(ntw))
-    order = [orig.index(C.cast(arr[i], C.c_void_p).value) for i in range(n)]
+    addrs = C.cast(arr, C.POINTER(C.c_void_p))
+    order = [orig[addrs[i]] for i in range(n)]
     return rc, list(tw)[: ntw.value], order, list(clens)
 
 

@@ -35,6 +35,7 @@ for s in "$@"; do
     bench-fill) step bench_fill 300 python bench.py --steps 200 --warmup 20 --mode fill --cpu-seconds 0 ;;
     bench-cfg3) step bench_cfg3 300 python bench.py --config cfg3 --steps 100 --warmup 10 --cpu-seconds 0 ;;
     bench-cfg4) step bench_cfg4 300 python bench.py --config cfg4 --steps 100 --warmup 10 --cpu-seconds 0 ;;
+    bench-gro) step bench_gro 300 python bench.py --config gro --steps 200 --warmup 20 --cpu-seconds 3 ;;
     bench-cfg5) step bench_cfg5 300 python bench.py --config cfg5 --steps 100 --warmup 10 --cpu-seconds 0 ;;
     prof) (cd /tmp && step prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e) ;;
     pmc) (cd /tmp && step pmc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e --no-event-timing) ;;

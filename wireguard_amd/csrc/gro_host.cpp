@@ -4,7 +4,9 @@
 //      and copied to HBM; checksumValid (gro.go:554-612) for every candidate
 //      is computed there by the batch VALIDATE kernel.  Validation always
 //      precedes mutation in the reference (gro.go:665-681, :709-723,
-//      :767-775), so precomputed validity bits are exact.
+//      :767-775), so precomputed validity bits are exact.  The plan (2) is
+//      made first assuming valid checksums and queued with the VALIDATE
+//      launch (one round trip); it is redone if a bit it used is false.
 //   2. the order-dependent flow-table decisions of tcpGRO / udpGRO
 //      (gro.go:801-1095: Go maps keyed by flow, sequence adjacency, PSH,
 //      capacity, prepend swaps) run here on the host, on headers and lengths
@@ -91,9 +93,15 @@ struct Planner {
   size_t* caps;
   int n, offset;
   std::vector<const uint8_t*> orig;   // original packet starts (host)
-  std::vector<uint8_t> valid;          // checksumValid per original index (GPU)
+  std::vector<uint8_t> valid;          // checksumValid per original index (GPU, or assumed)
+  std::vector<uint8_t> consulted;      // validity bits the decisions depended on
   std::vector<Content> content;        // per slot, swapped with bufs
   std::unordered_map<FlowKey, std::vector<Item>, FlowHash> tcp, udp;
+
+  bool V(int i) {  // checksumValid of the packet at slot i, recording that the plan used it
+    consulted[i] = 1;
+    return valid[i] != 0;
+  }
 
   // header bytes of the buffer now at `slot` (the head packet's original header)
   const uint8_t* head(int slot) const { return orig[content[slot].pieces[0].pkt]; }
@@ -164,8 +172,8 @@ struct Planner {
     if (mode == PREPEND) {
       if (caps[bi] - (size_t)offset < new_len) return INSUFF_CAP;
       if (psh) return PSH_ENDING;
-      if (it.num_merged == 0 && !valid[it.bufs_index]) return ITEM_BAD;
-      if (!valid[bi]) return PKT_BAD;
+      if (it.num_merged == 0 && !V(it.bufs_index)) return ITEM_BAD;
+      if (!V(bi)) return PKT_BAD;
       it.seq = seq;
       const size_t item_pay = new_len - pl;
       Content& dst = content[bi];
@@ -177,8 +185,8 @@ struct Planner {
       swap_slots(it.bufs_index, bi);  // gro.go:696-697
     } else {
       if (caps[it.bufs_index] - (size_t)offset < new_len) return INSUFF_CAP;
-      if (it.num_merged == 0 && !valid[it.bufs_index]) return ITEM_BAD;
-      if (!valid[bi]) return PKT_BAD;
+      if (it.num_merged == 0 && !V(it.bufs_index)) return ITEM_BAD;
+      if (!V(bi)) return PKT_BAD;
       if (psh) {
         it.psh = true;
         content[it.bufs_index].psh = true;  // pktHead[iphLen+13] |= PSH (gro.go:724-729)
@@ -292,8 +300,8 @@ struct Planner {
       const size_t pay = pl - hdrs;
       int r;
       if (caps[item.bufs_index] - (size_t)offset < tl + pay) r = INSUFF_CAP;
-      else if (item.num_merged == 0 && (item.csum_bad || !valid[item.bufs_index])) r = ITEM_BAD;
-      else if (!valid[bi]) r = PKT_BAD;
+      else if (item.num_merged == 0 && (item.csum_bad || !V(item.bufs_index))) r = ITEM_BAD;
+      else if (!V(bi)) r = PKT_BAD;
       else {
         content[item.bufs_index].pieces.push_back({bi, hdrs, (uint32_t)pay});
         lens[item.bufs_index] += pay;
@@ -329,8 +337,113 @@ int gro_candidate(const uint8_t* pkt, size_t len, bool can_udp) {
   return NOT_CAND;
 }
 
+// The host half of one handleGRO: flow decisions (gro.go:1334-1363) and the
+// applyTCPCoalesce / applyUDPCoalesce gather plan (:1364-1366) for the given
+// validity bits.  Nothing is written to the caller's bytes here (only the
+// bufs/lens/caps slice headers move, as the Go code moves them).
+struct Plan {
+  std::vector<int> to_write, zero_hdr;  // slots to write; slots whose virtio header is all-zero
+  std::vector<GroItem> items;
+  std::vector<GroSeg> segs;
+  std::vector<int> item_slot;
+  uint64_t out_bytes = 0;
+};
+
+void make_plan(Planner& P, const std::vector<int>& cand, const std::vector<uint64_t>& stage_off, Plan& out) {
+  const int n = P.n;
+  for (int i = 0; i < n; ++i) {
+    int res = NOOP;
+    switch (cand[i]) {
+      case TCP4: res = P.tcp_gro(i, false); break;
+      case TCP6: res = P.tcp_gro(i, true); break;
+      case UDP4: res = P.udp_gro(i, false); break;
+      case UDP6: res = P.udp_gro(i, true); break;
+    }
+    if (res == NOOP) out.zero_hdr.push_back(i);  // gro.go:1350-1358
+    if (res == NOOP || res == INSERT) out.to_write.push_back(i);
+  }
+  auto apply = [&](std::unordered_map<FlowKey, std::vector<Item>, FlowHash>& table, bool udp) {
+    for (auto& kv : table) {
+      for (const Item& it : kv.second) {
+        const int slot = it.bufs_index;
+        if (it.num_merged == 0) {
+          out.zero_hdr.push_back(slot);
+          continue;
+        }
+        const Content& c = P.content[slot];
+        GroItem gi;
+        memset(&gi, 0, sizeof gi);
+        gi.out_off = out.out_bytes;
+        gi.head_off = (uint32_t)stage_off[c.pieces[0].pkt];
+        gi.pkt_len = (uint32_t)(P.lens[slot] - P.offset);
+        gi.iph = it.iph;
+        gi.l4h = it.l4h;
+        gi.gso_size = it.gso_size;
+        gi.kind = (uint8_t)((it.key.v6 ? GRO_KIND_V6 : 0) | (udp ? GRO_KIND_UDP : 0) | (c.psh ? GRO_KIND_PSH : 0));
+        gi.seg_first = (uint32_t)out.segs.size();
+        const uint32_t hdr = (uint32_t)it.iph + it.l4h;
+        uint64_t dst = out.out_bytes + kVnetLen + hdr;
+        for (size_t k = 0; k < c.pieces.size(); ++k) {  // piece 0 = head packet; its header is rebuilt
+          Piece pc = c.pieces[k];
+          if (k == 0) {
+            pc.start += hdr;
+            pc.len -= hdr;
+          }
+          if (pc.len) out.segs.push_back({(uint32_t)(stage_off[pc.pkt] + pc.start), pc.len, (uint32_t)dst, 0u});
+          dst += pc.len;
+        }
+        gi.seg_count = (uint32_t)out.segs.size() - gi.seg_first;
+        out.items.push_back(gi);
+        out.item_slot.push_back(slot);
+        out.out_bytes += (kVnetLen + gi.pkt_len + 15) & ~(uint64_t)15;
+      }
+    }
+  };
+  apply(P.tcp, false);
+  apply(P.udp, true);
+}
+
+void init_planner(Planner& P, uint8_t** bufs, size_t* lens, size_t* caps, int n, int offset,
+                  const std::vector<const uint8_t*>& orig, const std::vector<uint8_t>& valid) {
+  P.bufs = bufs;
+  P.lens = lens;
+  P.caps = caps;
+  P.n = n;
+  P.offset = offset;
+  P.orig = orig;
+  P.valid = valid;
+  P.consulted.assign(n, 0);
+  P.content.assign(n, Content());
+  for (int i = 0; i < n; ++i) P.content[i].pieces.push_back({i, 0, (uint32_t)(lens[i] - offset)});
+}
+
+// Queue the coalesce plan on stream s: H2D of items + pieces, kernel, D2H.
+int queue_coalesce(wgcs_ctx* ctx, const Plan& pl, hipStream_t s) {
+  if (pl.items.empty()) return WGCS_OK;
+  const size_t ib = pl.items.size() * sizeof(GroItem), sb = std::max<size_t>(pl.segs.size(), 1) * sizeof(GroSeg);
+  int rc;
+  if ((rc = ensure_pinned(ctx, ctx->h_meta, ib + sb)) || (rc = ensure_dev(ctx, ctx->d_aux, ib + sb)) ||
+      (rc = ensure_dev(ctx, ctx->d_out, pl.out_bytes + 16)) || (rc = ensure_pinned(ctx, ctx->h_out, pl.out_bytes + 16)))
+    return rc;
+  memcpy(ctx->h_meta.ptr, pl.items.data(), ib);
+  memcpy((uint8_t*)ctx->h_meta.ptr + ib, pl.segs.data(), pl.segs.size() * sizeof(GroSeg));
+  hipError_t e = hipMemcpyAsync(ctx->d_aux.ptr, ctx->h_meta.ptr, ib + sb, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = launch_gro_coalesce((const uint8_t*)ctx->d_arena.ptr, (const GroItem*)ctx->d_aux.ptr,
+                            (uint32_t)pl.items.size(), (const GroSeg*)((uint8_t*)ctx->d_aux.ptr + ib),
+                            (uint32_t)pl.segs.size(), (uint8_t*)ctx->d_out.ptr, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->h_out.ptr, ctx->d_out.ptr, pl.out_bytes, hipMemcpyDeviceToHost, s);
+  return e == hipSuccess ? WGCS_OK : hip_fail(ctx, e, "GRO coalesce");
+}
+
 }  // namespace
 
+// handleGRO with one GPU round trip in the common case: the flow plan is made
+// assuming every candidate's checksum is valid and queued together with the
+// VALIDATE kernel; if any validity bit the plan consulted turns out false,
+// the slice headers are restored and the plan is redone with the real bits
+// (a second round trip).  Results are therefore always those of the
+// reference's order of checks (gro.go:665-681, :709-723, :767-775).
 extern "C" int wgcs_handle_gro(wgcs_ctx* ctx, uint8_t** bufs, size_t* lens, size_t* caps, int n, int offset,
                                int can_udp_gro, int* to_write, int* n_to_write) {
   if (!ctx || !n_to_write || (n > 0 && (!bufs || !lens || !caps || !to_write))) return WGCS_ERR_INVALID_ARG;
@@ -340,54 +453,56 @@ extern "C" int wgcs_handle_gro(wgcs_ctx* ctx, uint8_t** bufs, size_t* lens, size
     if (offset < kVnetLen || (long)offset > (long)lens[i] - 1)
       return set_err(ctx, WGCS_ERR_INVALID_OFFSET, "invalid offset (packet %d)", i);
 
-  Planner P;
-  P.bufs = bufs;
-  P.lens = lens;
-  P.caps = caps;
-  P.n = n;
-  P.offset = offset;
-  P.orig.resize(n);
-  P.valid.assign(n, 0);
-  P.content.resize(n);
+  std::vector<const uint8_t*> orig(n);
   std::vector<int> cand(n);
   std::vector<uint64_t> stage_off(n, 0);
+  std::vector<uint8_t> assume(n, 0);
   uint64_t stage_bytes = 0;
   uint32_t ncand = 0;
   for (int i = 0; i < n; ++i) {
-    P.orig[i] = bufs[i] + offset;
-    P.content[i].pieces.push_back({i, 0, (uint32_t)(lens[i] - offset)});
-    cand[i] = gro_candidate(P.orig[i], lens[i] - offset, can_udp_gro != 0);
+    orig[i] = bufs[i] + offset;
+    cand[i] = gro_candidate(orig[i], lens[i] - offset, can_udp_gro != 0);
     if (cand[i] != NOT_CAND) {
       stage_off[i] = stage_bytes;
       stage_bytes += (lens[i] - offset + 15) & ~(size_t)15;
+      assume[i] = 1;
       ++ncand;
     }
   }
+  // slice headers as the caller passed them (restored if the plan is redone)
+  const std::vector<uint8_t*> bufs0(bufs, bufs + n);
+  const std::vector<size_t> lens0(lens, lens + n), caps0(caps, caps + n);
+
+  Planner P;
+  init_planner(P, bufs, lens, caps, n, offset, orig, assume);
+  Plan pl;
+  make_plan(P, cand, stage_off, pl);
 
   std::lock_guard<std::mutex> g(ctx->mu);
   hipSetDevice(ctx->device);
   hipStream_t s = ctx->stream;
   int rc;
+  std::vector<uint8_t> real(n, 0);
   if (ncand) {
-    // ---- 1. stage candidates, checksumValid on the GPU
+    // ---- one submission: stage candidates, VALIDATE, coalesce (speculative plan), D2H
     const size_t meta = (size_t)ncand * sizeof(wgcs_pkt);
-    if ((rc = ensure_pinned(ctx, ctx->h_stage, stage_bytes + 16)) || (rc = ensure_pinned(ctx, ctx->h_meta, meta)) ||
-        (rc = ensure_pinned(ctx, ctx->h_out, ncand)) || (rc = ensure_dev(ctx, ctx->d_arena, stage_bytes + 16)) ||
-        (rc = ensure_dev(ctx, ctx->d_pkts, meta)) || (rc = ensure_dev(ctx, ctx->d_init, ncand)))
+    if ((rc = ensure_pinned(ctx, ctx->h_stage, stage_bytes + 16 + meta + ncand)) ||
+        (rc = ensure_dev(ctx, ctx->d_arena, stage_bytes + 16)) || (rc = ensure_dev(ctx, ctx->d_pkts, meta)) ||
+        (rc = ensure_dev(ctx, ctx->d_init, ncand)))
       return rc;
     uint8_t* hs = (uint8_t*)ctx->h_stage.ptr;
-    wgcs_pkt* hp = (wgcs_pkt*)ctx->h_meta.ptr;
+    wgcs_pkt* hp = (wgcs_pkt*)(hs + ((stage_bytes + 15) & ~(size_t)15));
+    uint8_t* hv = (uint8_t*)(hp + ncand);
     std::vector<int> cidx;
     cidx.reserve(ncand);
     for (int i = 0; i < n; ++i) {
       if (cand[i] == NOT_CAND) continue;
-      const size_t pl = lens[i] - offset;
-      memcpy(hs + stage_off[i], P.orig[i], pl);
+      memcpy(hs + stage_off[i], orig[i], lens0[i] - offset);
       const bool v6 = cand[i] == TCP6 || cand[i] == UDP6;
       const bool udp = cand[i] == UDP4 || cand[i] == UDP6;
       wgcs_pkt d;
       d.off = stage_off[i];
-      d.len = (uint32_t)pl;
+      d.len = (uint32_t)(lens0[i] - offset);
       d.csum_start = (uint16_t)(v6 ? 40 : 20);  // item.iphLen (IHL 5 for IPv4 candidates)
       d.csum_offset = 0;
       d.flags = (uint8_t)((v6 ? WGCS_PKT_V6 : 0) | (udp ? WGCS_PKT_UDP : 0));
@@ -396,90 +511,37 @@ extern "C" int wgcs_handle_gro(wgcs_ctx* ctx, uint8_t** bufs, size_t* lens, size
     }
     hipError_t e = hipMemcpyAsync(ctx->d_arena.ptr, hs, stage_bytes, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(ctx->d_pkts.ptr, hp, meta, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return hip_fail(ctx, e, "GRO H2D");
-    e = launch_checksum_batch(WGCS_MODE_VALIDATE, 0, (uint8_t*)ctx->d_arena.ptr, (const wgcs_pkt*)ctx->d_pkts.ptr,
-                              nullptr, ncand, ctx->d_init.ptr, s, ctx->num_cu, ctx->tune);
-    if (e == hipSuccess) e = hipMemcpyAsync(ctx->h_out.ptr, ctx->d_init.ptr, ncand, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess)
+      e = launch_checksum_batch(WGCS_MODE_VALIDATE, 0, (uint8_t*)ctx->d_arena.ptr, (const wgcs_pkt*)ctx->d_pkts.ptr,
+                                nullptr, ncand, ctx->d_init.ptr, s, ctx->num_cu, ctx->tune);
+    if (e == hipSuccess) e = hipMemcpyAsync(hv, ctx->d_init.ptr, ncand, hipMemcpyDeviceToHost, s);
     if (e != hipSuccess) return hip_fail(ctx, e, "GRO validate");
-    for (uint32_t k = 0; k < ncand; ++k) P.valid[cidx[k]] = ((uint8_t*)ctx->h_out.ptr)[k];
+    if ((rc = queue_coalesce(ctx, pl, s))) return rc;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "GRO sync");
+    for (uint32_t k = 0; k < ncand; ++k) real[cidx[k]] = hv[k];
+    bool redo = false;
+    for (int i = 0; i < n && !redo; ++i) redo = P.consulted[i] && !real[i];
+    if (redo) {  // mis-speculated: restore the slice headers, plan with the real bits
+      std::copy(bufs0.begin(), bufs0.end(), bufs);
+      std::copy(lens0.begin(), lens0.end(), lens);
+      std::copy(caps0.begin(), caps0.end(), caps);
+      Planner Q;
+      init_planner(Q, bufs, lens, caps, n, offset, orig, real);
+      pl = Plan();
+      make_plan(Q, cand, stage_off, pl);
+      if ((rc = queue_coalesce(ctx, pl, s))) return rc;
+      if (!pl.items.empty() && (e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "GRO sync");
+    }
   }
 
-  // ---- 2. flow-table decisions (gro.go:1334-1363), headers and lengths only
+  // ---- apply: empty virtio headers, coalesced super-packets, toWrite
   static const uint8_t zero_hdr[kVnetLen] = {0};
-  for (int i = 0; i < n; ++i) {
-    int res = NOOP;
-    switch (cand[i]) {
-      case TCP4: res = P.tcp_gro(i, false); break;
-      case TCP6: res = P.tcp_gro(i, true); break;
-      case UDP4: res = P.udp_gro(i, false); break;
-      case UDP6: res = P.udp_gro(i, true); break;
-    }
-    if (res == NOOP) memcpy(bufs[i] + offset - kVnetLen, zero_hdr, kVnetLen);  // gro.go:1350-1358
-    if (res == NOOP || res == INSERT) to_write[(*n_to_write)++] = i;
+  for (int slot : pl.zero_hdr) memcpy(bufs[slot] + offset - kVnetLen, zero_hdr, kVnetLen);
+  for (size_t k = 0; k < pl.items.size(); ++k) {
+    const int slot = pl.item_slot[k];
+    memcpy(bufs[slot] + offset - kVnetLen, (uint8_t*)ctx->h_out.ptr + pl.items[k].out_off,
+           kVnetLen + pl.items[k].pkt_len);
   }
-
-  // ---- 3. applyTCPCoalesce / applyUDPCoalesce (gro.go:1364-1366)
-  std::vector<GroItem> items;
-  std::vector<GroSeg> segs;
-  std::vector<int> item_slot;
-  uint64_t out_bytes = 0;
-  auto apply = [&](std::unordered_map<FlowKey, std::vector<Item>, FlowHash>& table, bool udp) {
-    for (auto& kv : table) {
-      for (const Item& it : kv.second) {
-        const int slot = it.bufs_index;
-        if (it.num_merged == 0) {
-          memcpy(bufs[slot] + offset - kVnetLen, zero_hdr, kVnetLen);
-          continue;
-        }
-        const Content& c = P.content[slot];
-        GroItem gi;
-        memset(&gi, 0, sizeof gi);
-        gi.out_off = out_bytes;
-        gi.head_off = (uint32_t)stage_off[c.pieces[0].pkt];
-        gi.pkt_len = (uint32_t)(lens[slot] - offset);
-        gi.iph = it.iph;
-        gi.l4h = it.l4h;
-        gi.gso_size = it.gso_size;
-        gi.kind = (uint8_t)((it.key.v6 ? GRO_KIND_V6 : 0) | (udp ? GRO_KIND_UDP : 0) | (c.psh ? GRO_KIND_PSH : 0));
-        gi.seg_first = (uint32_t)segs.size();
-        const uint32_t hdr = (uint32_t)it.iph + it.l4h;
-        for (size_t k = 0; k < c.pieces.size(); ++k) {  // piece 0 = head packet; its header is rebuilt
-          Piece pc = c.pieces[k];
-          if (k == 0) {
-            pc.start += hdr;
-            pc.len -= hdr;
-          }
-          if (pc.len) segs.push_back({(uint32_t)(stage_off[pc.pkt] + pc.start), pc.len});
-        }
-        gi.seg_count = (uint32_t)segs.size() - gi.seg_first;
-        items.push_back(gi);
-        item_slot.push_back(slot);
-        out_bytes += (kVnetLen + gi.pkt_len + 15) & ~(uint64_t)15;
-      }
-    }
-  };
-  apply(P.tcp, false);
-  apply(P.udp, true);
-  if (items.empty()) return WGCS_OK;
-
-  // ---- GPU gather + header rewrite of every merged super-packet
-  const size_t ib = items.size() * sizeof(GroItem), sb = std::max<size_t>(segs.size(), 1) * sizeof(GroSeg);
-  if ((rc = ensure_pinned(ctx, ctx->h_meta, ib + sb)) || (rc = ensure_dev(ctx, ctx->d_aux, ib + sb)) ||
-      (rc = ensure_dev(ctx, ctx->d_out, out_bytes + 16)) || (rc = ensure_pinned(ctx, ctx->h_out, out_bytes + 16)))
-    return rc;
-  memcpy(ctx->h_meta.ptr, items.data(), ib);
-  memcpy((uint8_t*)ctx->h_meta.ptr + ib, segs.data(), segs.size() * sizeof(GroSeg));
-  hipError_t e = hipMemcpyAsync(ctx->d_aux.ptr, ctx->h_meta.ptr, ib + sb, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess)
-    e = launch_gro_coalesce((const uint8_t*)ctx->d_arena.ptr, (const GroItem*)ctx->d_aux.ptr, (uint32_t)items.size(),
-                            (const GroSeg*)((uint8_t*)ctx->d_aux.ptr + ib), (uint8_t*)ctx->d_out.ptr, s, ctx->num_cu);
-  if (e == hipSuccess) e = hipMemcpyAsync(ctx->h_out.ptr, ctx->d_out.ptr, out_bytes, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return hip_fail(ctx, e, "GRO coalesce");
-  for (size_t k = 0; k < items.size(); ++k) {
-    const int slot = item_slot[k];
-    memcpy(bufs[slot] + offset - kVnetLen, (uint8_t*)ctx->h_out.ptr + items[k].out_off, kVnetLen + items[k].pkt_len);
-  }
+  for (int i : pl.to_write) to_write[(*n_to_write)++] = i;
   return WGCS_OK;
 }

@@ -9,8 +9,9 @@
 // applyTCPCoalesce / applyUDPCoalesce (gro.go:1099-1268): IPv4 total length +
 // header checksum or IPv6 payload length, UDP length, PSH, the virtio header,
 // and the uncomplemented pseudo-header checksum in the L4 checksum field.
-// One wave64 per output item; payload pieces are copied with aligned 16-byte
-// loads/stores (wgcs_copy.h).
+// One wave64 per output item header and one per payload piece (the host
+// computes every piece's destination), so an item's pieces copy in parallel;
+// pieces move with aligned 16-byte loads/stores (wgcs_copy.h).
 #include <hip/hip_runtime.h>
 
 #include "../../include/wgcsum.h"
@@ -56,12 +57,20 @@ __device__ __forceinline__ uint32_t patched(const uint8_t* head, const HdrPatch&
 
 __global__ __launch_bounds__(256) void gro_coalesce_kernel(const uint8_t* __restrict__ stage,
                                                            const GroItem* __restrict__ items, uint32_t n_items,
-                                                           const GroSeg* __restrict__ segs,
+                                                           const GroSeg* __restrict__ segs, uint32_t n_segs,
                                                            uint8_t* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-  const uint32_t nwaves = gridDim.x * 4;
-  for (uint32_t it = wave; it < n_items; it += nwaves) {
+  if (wave >= n_items) {  // payload piece (coalesceTCPPackets / coalesceUDPPackets appends, gro.go:630-783)
+    const uint32_t k = wave - n_items;
+    if (k < n_segs) {
+      const GroSeg sg = segs[k];
+      copy_range(stage + sg.src_off, (int)sg.len, out + sg.dst_off, lane);
+    }
+    return;
+  }
+  {
+    const uint32_t it = wave;
     const GroItem g = items[it];
     const uint8_t* head = stage + g.head_off;
     HdrPatch h;
@@ -103,22 +112,14 @@ __global__ __launch_bounds__(256) void gro_coalesce_kernel(const uint8_t* __rest
       if (x == h.csum_at + 1) b = pcs & 0xFF;
       o[10 + x] = (uint8_t)b;
     }
-    // payload pieces in coalesced order
-    long cur = 10 + h.hdr_len;
-    for (uint32_t k = 0; k < g.seg_count; ++k) {
-      const GroSeg sg = segs[g.seg_first + k];
-      copy_range(stage + sg.src_off, (int)sg.len, o + cur, lane);
-      cur += sg.len;
-    }
   }
 }
 
 hipError_t launch_gro_coalesce(const uint8_t* stage, const GroItem* items, uint32_t n_items, const GroSeg* segs,
-                               uint8_t* out, hipStream_t s, int num_cu) {
+                               uint32_t n_segs, uint8_t* out, hipStream_t s) {
   if (n_items == 0) return hipSuccess;
-  uint32_t grid = (n_items + 3) / 4;
-  if (grid > (uint32_t)num_cu * 4) grid = (uint32_t)num_cu * 4;
-  hipLaunchKernelGGL(gro_coalesce_kernel, dim3(grid), dim3(256), 0, s, stage, items, n_items, segs, out);
+  const uint32_t grid = (n_items + n_segs + 3) / 4;  // one wave per item header + one per piece
+  hipLaunchKernelGGL(gro_coalesce_kernel, dim3(grid), dim3(256), 0, s, stage, items, n_items, segs, n_segs, out);
   return hipGetLastError();
 }
 

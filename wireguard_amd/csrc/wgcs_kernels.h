@@ -47,10 +47,11 @@ struct GroItem {
 };
 struct GroSeg {
   uint32_t src_off, len;  // stage offset / length of one payload piece
+  uint32_t dst_off, pad;  // output offset of the piece (host-computed: pieces copy in parallel)
 };
 enum : uint8_t { GRO_KIND_V6 = 1, GRO_KIND_UDP = 2, GRO_KIND_PSH = 4 };
 
 hipError_t launch_gro_coalesce(const uint8_t* stage, const GroItem* items, uint32_t n_items, const GroSeg* segs,
-                               uint8_t* out, hipStream_t s, int num_cu);
+                               uint32_t n_segs, uint8_t* out, hipStream_t s);
 
 }  // namespace wgcs

@@ -1,0 +1,147 @@
+"""Tun.Write measurement: handleGRO
+(tun/gro.go:1326-1367) over one device.RoutineSendToInternet batch of 128
+packets from host buffers, the reference's Write granularity (conn/conn.go:12-15).
+Called by bench.py --config gro.
+
+Batch: 4 TCP/IPv4 flows x 32 in-order 1448-B MSS segments (1488-B packets), the
+common bulk-transfer case; every segment coalesces into 4 packets of 32 x 1448 B.
+One step = one wgcs_handle_gro C call (argument arrays prebuilt): stage into
+pinned memory, H2D, the VALIDATE checksum kernel, the host flow planner, the
+coalesce kernel, D2H and the copy back into the Go-slice buffers.
+Unit: packets/s (higher is better).
+"""
+from __future__ import annotations
+
+import json
+import time
+
+import numpy as np
+
+from . import synth
+
+OFFSET = 16
+CAP = 65535 + OFFSET
+
+
+def make_batch(dev, flows: int = 4, per_flow: int = 32, mss: int = 1448, seed: int = synth.SEED):
+    """128 segmented TCP/IPv4 packets, produced by the product's GSO split of
+    one super-packet per flow (flows interleaved round-robin, in order per flow)."""
+    segs = []
+    for f in range(flows):
+        vp = synth.make_super_packet(40 + per_flow * mss, mss, seed=seed + f, tcp_flags=0x10)
+        bufs = [np.zeros(mss + 200, np.uint8) for _ in range(per_flow + 2)]
+        sizes = [0] * len(bufs)
+        n, err = dev.handle_virtio_read(np.frombuffer(bytearray(vp), np.uint8).copy(), bufs, sizes, OFFSET)
+        assert err is None and n == per_flow, (n, err)
+        segs.append([bufs[i][OFFSET: OFFSET + sizes[i]].tobytes() for i in range(n)])
+    return [segs[f][k] for k in range(per_flow) for f in range(flows)]
+
+
+class Batch:
+    """The 128 packets as Go-slice style buffers (cap CAP, len OFFSET+len(p))
+    inside one arena, with the C argument arrays prebuilt, so a timed step is
+    exactly one C call; reset() restores bytes, pointers and lengths."""
+
+    def __init__(self, pkts):
+        import ctypes as C
+
+        self.C = C
+        n = len(pkts)
+        self.n = n
+        self.arena = np.zeros((n, CAP), np.uint8)
+        self.orig = np.zeros((n, OFFSET + max(len(p) for p in pkts) + 16), np.uint8)
+        for i, p in enumerate(pkts):
+            self.orig[i, OFFSET: OFFSET + len(p)] = np.frombuffer(p, np.uint8)
+        u8p = C.POINTER(C.c_uint8)
+        self.ptrs0 = (u8p * n)(*[C.cast(self.arena[i].ctypes.data, u8p) for i in range(n)])
+        self.ptrs = (u8p * n)()
+        self.lens0 = (C.c_size_t * n)(*[OFFSET + len(p) for p in pkts])
+        self.lens = (C.c_size_t * n)()
+        self.caps = (C.c_size_t * n)(*([CAP] * n))
+        self.tw = (C.c_int * n)()
+        self.ntw = C.c_int(0)
+        self.width = self.orig.shape[1]
+
+    def reset(self):
+        C = self.C
+        self.arena[:, : self.width] = self.orig
+        C.memmove(self.ptrs, self.ptrs0, C.sizeof(self.ptrs0))
+        C.memmove(self.lens, self.lens0, C.sizeof(self.lens0))
+
+
+def run(args, torch, dev, dist, rank, world, local, barrier):
+    pkts = make_batch(dev)
+    n = len(pkts)
+    payload = sum(len(p) for p in pkts)
+    b = Batch(pkts)
+    L, h = dev.lib, dev.h
+
+    def call():
+        return L.wgcs_handle_gro(h, b.ptrs, b.lens, b.caps, b.n, OFFSET, 1, b.tw, b.C.byref(b.ntw))
+
+    for _ in range(args.warmup):
+        b.reset()
+        assert call() == 0 and b.ntw.value == 4, b.ntw.value
+    barrier()
+    t_total = 0.0
+    for _ in range(args.steps):
+        b.reset()  # Write gets fresh bufs: restored outside the timed call
+        t0 = time.perf_counter()
+        call()
+        t_total += time.perf_counter() - t0
+    barrier()
+    if dist is not None:
+        t = torch.tensor([t_total], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_total = float(t.item())
+    per = t_total / args.steps
+    result = {
+        "metric": "Tun.Write handleGRO packets/s (host buffers, 128-packet batch)",
+        "value": round(n * world / per, 1),
+        "unit": "packets/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(per * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {
+            "workload": "128 TCP/IPv4 packets (4 flows x 32 x 1448-B MSS) per wgcs_handle_gro call, "
+                        "coalesced to 4 packets; host buffers in and out",
+            "packets_per_step": n,
+            "payload_bytes": payload,
+            "parallelism": f"replica{world} (one context per GPU, no collective)",
+            "gib_per_s": round(payload / per / 2**30, 3),
+        },
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        result["cpu_baseline"] = cpu_baseline(pkts, min(args.cpu_seconds, 5.0))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    dev.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(pkts, seconds):
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import oracle  # cpu_baseline leg only
+
+    b = Batch(pkts)
+    L = oracle.lib()
+    reps, t_total = 0, 0.0
+    while t_total < seconds:
+        b.reset()
+        t0 = time.perf_counter()
+        L.or_handle_gro(b.ptrs, b.lens, b.caps, b.n, OFFSET, 1, b.tw, b.C.byref(b.ntw))
+        t_total += time.perf_counter() - t0
+        reps += 1
+    return {"value": round(len(pkts) * reps / t_total, 1), "unit": "packets/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} handleGRO calls on the same 128-packet batch, {t_total:.1f} s, "
+                      "C restatement of tun/gro.go, one C call per step (as the product is timed)"}

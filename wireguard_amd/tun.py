@@ -193,13 +193,14 @@ class Device:
         arr = (u8p * n)()
         for i, b in enumerate(bufs):
             arr[i] = C.cast(b.ctypes.data, u8p)
-        orig = [C.cast(arr[i], C.c_void_p).value for i in range(n)]
+        orig = {b.ctypes.data: i for i, b in enumerate(bufs)}
         clens = (C.c_size_t * n)(*lens)
         ccaps = (C.c_size_t * n)(*[len(b) for b in bufs])
         tw = (C.c_int * max(n, 1))()
         ntw = C.c_int(0)
         rc = self.lib.wgcs_handle_gro(self.h, arr, clens, ccaps, n, offset, int(can_udp_gro), tw, C.byref(ntw))
-        order = [orig.index(C.cast(arr[i], C.c_void_p).value) for i in range(n)]
+        addrs = C.cast(arr, C.POINTER(C.c_void_p))
+        order = [orig[addrs[i]] for i in range(n)]
         return list(tw)[: ntw.value], order, list(clens), self._err(rc)
 
 
