@@ -25,45 +25,59 @@ struct GsoResult {
   int count = 0;
 };
 
-// Runs one job through the kernel with bufs as the output slots.
-// vbuf = [10-byte virtio header | packet bytes] in host memory.
-// Caller holds ctx->mu (vbuf may be the context's own pinned staging).
+// Runs one job through the kernel and copies its segments into bufs.
+// vbuf = [10-byte virtio header | packet bytes] in host memory.  One round
+// trip: the segments land in a packed device region whose size the host
+// bounds from the virtio header (gso_out_layout), so the D2H of the segments
+// is queued with the launch instead of after a read-back of their sizes.
+// The room checks use bufs[0]'s room, as the reference does (tun/tun.go:546,
+// gro.go:1406-1410); other buffers are checked when copying, where the Go
+// code would panic on the slice.  Caller holds ctx->mu (vbuf may be the
+// context's own pinned staging).
 int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflags, uint8_t* const* bufs,
                  const size_t* buf_lens, int nbufs, int* sizes, int offset, GsoResult* res) {
   if (nbufs <= 0 || !bufs || !buf_lens || !sizes || offset < 0)
     return set_err(ctx, WGCS_ERR_INVALID_ARG, "bufs/sizes/offset");
   if (vlen > 0x7FFFFFF0u) return set_err(ctx, WGCS_ERR_INVALID_ARG, "super-packet too large");
   if (buf_lens[0] < (size_t)offset) return set_err(ctx, WGCS_ERR_OUT_OF_RANGE, "offset beyond bufs[0]");
-  // Device slots mirror bufs[0]'s capacity (the reference's room check for
-  // GSO_NONE is against bufs[0]); other buffers are checked after the kernel.
-  const size_t stride = std::min<size_t>(buf_lens[0], (size_t)offset + std::max<size_t>(vlen, 16));
+  const size_t room = std::min<size_t>(buf_lens[0] - (size_t)offset, 0xFFFFFFFFu);
+  uint32_t pitch, nseg_bound;
+  gso_out_layout(vbuf, vlen, (uint32_t)nbufs, &pitch, &nseg_bound);
+  if (pitch == 0) pitch = 16;
+  const size_t region = (size_t)pitch * nseg_bound;
   hipSetDevice(ctx->device);
   int rc;
-  const size_t meta = (size_t)nbufs * 4 + 16;
-  if ((rc = ensure_dev(ctx, ctx->d_arena, vlen + 32)) || (rc = ensure_dev(ctx, ctx->d_aux, sizeof(wgcs_gso_job))) ||
-      (rc = ensure_dev(ctx, ctx->d_out, (size_t)nbufs * stride + 16)) || (rc = ensure_dev(ctx, ctx->d_out2, meta)) ||
-      (rc = ensure_pinned(ctx, ctx->h_meta, meta + sizeof(wgcs_gso_job))))
+  const size_t meta = (size_t)nbufs * 4 + 16;  // sizes[nbufs] | count | status
+  const size_t aux = sizeof(wgcs_gso_job) + sizeof(GsoOutPos);
+  if ((rc = ensure_dev(ctx, ctx->d_arena, vlen + 32)) || (rc = ensure_dev(ctx, ctx->d_aux, aux)) ||
+      (rc = ensure_dev(ctx, ctx->d_out, region + 16)) || (rc = ensure_dev(ctx, ctx->d_out2, meta)) ||
+      (rc = ensure_pinned(ctx, ctx->h_meta, meta + aux)) || (rc = ensure_pinned(ctx, ctx->h_stage, region + 16)))
     return rc;
   hipStream_t s = ctx->stream;
-  wgcs_gso_job* hjob = (wgcs_gso_job*)((uint8_t*)ctx->h_meta.ptr + meta);
+  uint8_t* hm = (uint8_t*)ctx->h_meta.ptr;
+  wgcs_gso_job* hjob = (wgcs_gso_job*)(hm + meta);
+  GsoOutPos* hpos = (GsoOutPos*)(hjob + 1);
   hjob->off = 0;
   hjob->len = (uint32_t)vlen;
   hjob->flags = jflags;
+  hpos->base = 0;
+  hpos->pitch = pitch;
+  hpos->pad = 0;
   int32_t* d_sizes = (int32_t*)ctx->d_out2.ptr;
   int32_t* d_count = d_sizes + nbufs;
   int32_t* d_status = d_count + 1;
   hipError_t e = hipMemcpyAsync(ctx->d_arena.ptr, vbuf, vlen, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(ctx->d_aux.ptr, hjob, sizeof(wgcs_gso_job), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemsetAsync(d_sizes, 0, meta, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(ctx->d_aux.ptr, hjob, aux, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return hip_fail(ctx, e, "H2D");
   e = launch_gso_split_batch((const uint8_t*)ctx->d_arena.ptr, (const wgcs_gso_job*)ctx->d_aux.ptr, 1,
-                             (uint8_t*)ctx->d_out.ptr, (uint32_t)stride, (uint32_t)offset, (uint32_t)nbufs, d_sizes,
-                             d_count, d_status, s);
+                             (uint8_t*)ctx->d_out.ptr, 0, 0, (uint32_t)nbufs, d_sizes, d_count, d_status, s,
+                             (const GsoOutPos*)((uint8_t*)ctx->d_aux.ptr + sizeof(wgcs_gso_job)), (uint32_t)room);
   if (e != hipSuccess) return hip_fail(ctx, e, "gso_split launch");
-  int32_t* h = (int32_t*)ctx->h_meta.ptr;
+  int32_t* h = (int32_t*)hm;
   e = hipMemcpyAsync(h, d_sizes, meta, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && region) e = hipMemcpyAsync(ctx->h_stage.ptr, ctx->d_out.ptr, region, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return hip_fail(ctx, e, "D2H meta");
+  if (e != hipSuccess) return hip_fail(ctx, e, "D2H");
   res->count = h[nbufs];
   res->status = h[nbufs + 1];
   if (res->status != 0 && res->status != WGCS_ERR_TOO_MANY_SEGMENTS) {
@@ -71,15 +85,6 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
     return WGCS_OK;
   }
   const int written = res->status == WGCS_ERR_TOO_MANY_SEGMENTS ? nbufs : res->count;
-  if (written <= 0) return WGCS_OK;
-  int maxsz = 0;
-  for (int i = 0; i < written; ++i) maxsz = std::max(maxsz, (int)h[i]);
-  const size_t width = (size_t)maxsz;
-  if ((rc = ensure_pinned(ctx, ctx->h_stage, (size_t)written * std::max<size_t>(width, 1)))) return rc;
-  e = hipMemcpy2DAsync(ctx->h_stage.ptr, std::max<size_t>(width, 1), (uint8_t*)ctx->d_out.ptr + offset, stride,
-                       width, (size_t)written, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return hip_fail(ctx, e, "D2H segments");
   for (int i = 0; i < written; ++i) {
     sizes[i] = h[i];
     if (buf_lens[i] < (size_t)offset + (size_t)h[i]) {  // the Go code would panic on this slice
@@ -87,7 +92,7 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
       res->count = i;
       return WGCS_OK;
     }
-    memcpy(bufs[i] + offset, (uint8_t*)ctx->h_stage.ptr + (size_t)i * std::max<size_t>(width, 1), (size_t)h[i]);
+    memcpy(bufs[i] + offset, (const uint8_t*)ctx->h_stage.ptr + (size_t)i * pitch, (size_t)h[i]);
   }
   return WGCS_OK;
 }

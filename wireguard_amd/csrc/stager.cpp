@@ -34,8 +34,6 @@ using namespace wgcs;
 
 namespace {
 
-constexpr uint32_t kMaxHdr = 240;  // gso_rows_kernel's header limit (larger headers fail OUT_OF_RANGE)
-
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 struct Slot {
@@ -114,26 +112,6 @@ int open_slot(wgcs_stager* st, uint32_t idx) {
   return WGCS_OK;
 }
 
-// Output pitch / segment bound for one read from its virtio header: large
-// enough for every segment the kernel can write for it (or 0 if it writes none).
-void out_layout(const uint8_t* rb, size_t n, uint32_t max_segs, uint32_t* pitch, uint32_t* segs) {
-  *pitch = 0;
-  *segs = 0;
-  if (n <= 10) return;  // short buffer / empty packet: nothing written
-  const size_t plen = n - 10;
-  const uint8_t gso_type = rb[1];
-  uint16_t gso;
-  memcpy(&gso, rb + 4, 2);
-  if (gso_type == 0) {  // GSO_NONE: the packet itself
-    *pitch = (uint32_t)align16(plen);
-    *segs = 1;
-    return;
-  }
-  *pitch = (uint32_t)align16(kMaxHdr + (size_t)gso);
-  const size_t nseg = gso ? (plen + gso - 1) / gso + 1 : (size_t)max_segs;
-  *segs = (uint32_t)std::min<size_t>(nseg, max_segs);
-}
-
 int stage(wgcs_stager* st, size_t max_n, uint8_t** dst, int* read_idx) {
   Slot& s = st->slots[st->open];
   if (s.reserved >= 0) return set_err(st->ctx, WGCS_ERR_INVALID_ARG, "stager: commit the open reservation first");
@@ -148,7 +126,7 @@ int stage(wgcs_stager* st, size_t max_n, uint8_t** dst, int* read_idx) {
 int finish(wgcs_stager* st, size_t n) {
   Slot& s = st->slots[st->open];
   uint32_t pitch, segs;
-  out_layout(s.h_in + s.used_in, n, st->max_segs, &pitch, &segs);
+  gso_out_layout(s.h_in + s.used_in, n, st->max_segs, &pitch, &segs);
   const size_t region = (size_t)pitch * segs;
   if (s.used_out + region > st->max_out)
     return set_err(st->ctx, WGCS_ERR_BATCH_FULL, "stager: output region of the open batch is full");

@@ -29,6 +29,26 @@ struct GsoOutPos {
   uint32_t pitch;
   uint32_t pad;
 };
+// Packed-layout pitch and segment bound of one job ([10-byte virtio header |
+// packet], n bytes) from its virtio header: every segment gso_rows_kernel can
+// write for it fits in `pitch` (headers above 240 bytes fail OUT_OF_RANGE),
+// and it writes at most `segs` of them; 0/0 when it writes none.
+inline void gso_out_layout(const uint8_t* vb, size_t n, uint32_t max_segs, uint32_t* pitch, uint32_t* segs) {
+  *pitch = 0;
+  *segs = 0;
+  if (n <= 10) return;  // short buffer / empty packet: nothing written
+  const size_t plen = n - 10;
+  const uint32_t gso = (uint32_t)vb[4] | ((uint32_t)vb[5] << 8);
+  if (vb[1] == 0) {  // GSO_NONE: the packet itself
+    *pitch = (uint32_t)((plen + 15) & ~(size_t)15);
+    *segs = 1;
+    return;
+  }
+  *pitch = (240u + gso + 15u) & ~15u;
+  const size_t nseg = gso ? (plen + gso - 1) / gso + 1 : (size_t)max_segs;
+  *segs = (uint32_t)(nseg < max_segs ? nseg : max_segs);
+}
+
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs,
                                   uint8_t* out, uint32_t out_stride, uint32_t offset, uint32_t max_segs,
                                   int32_t* sizes, int32_t* count, int32_t* status,

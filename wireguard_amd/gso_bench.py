@@ -120,6 +120,7 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
     }
     if not getattr(args, "no_e2e", False):
         result["end_to_end"] = end_to_end(dev, pkts, bytes_in, bytes_out, steps=max(10, min(args.steps, 40)))
+        result["host_call"] = host_call(dev, pkts[0], with_cpu=rank == 0 and world == 1 and args.cpu_seconds > 0)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(pkts, args.cpu_seconds, bytes_per_step)
     if rank == 0:
@@ -163,6 +164,49 @@ def end_to_end(dev, pkts, bytes_in, bytes_out, steps: int, depth: int = 3):
             "ms_per_batch": round(dt * 1e3, 4), "bytes_in_plus_out": bytes_in + bytes_out,
             "what": f"Tun.Read stager, depth {depth}: host memcpy of the reads into pinned staging + H2D + "
                     "split kernel + D2H of the packed segments (PCIe-inclusive)"}
+
+
+def host_call(dev, vp: bytes, with_cpu: bool, reps: int = 200):
+    """Latency of one reference-shaped call, wgcs_handle_virtio_read on one
+    65,535-B read (Tun.Read granularity, host buffers in and out), as one C
+    call with prebuilt arguments; the oracle's time for the same call beside it."""
+    import ctypes as C
+
+    nb = 64
+    bufs = [np.zeros(1536, np.uint8) for _ in range(nb)]
+    u8p = C.POINTER(C.c_uint8)
+    arr = (u8p * nb)(*[C.cast(b.ctypes.data, u8p) for b in bufs])
+    lens = (C.c_size_t * nb)(*([1536] * nb))
+    sizes = (C.c_int * nb)()
+    n = C.c_int(0)
+    src = np.frombuffer(vp, np.uint8)
+    rb = src.copy()
+
+    def timed(fn):
+        ts = []
+        for _ in range(reps):
+            rb[:] = src  # handleVirtioRead edits readBuf in place: restore outside the timed call
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
+    L, h = dev.lib, dev.h
+    gpu = timed(lambda: L.wgcs_handle_virtio_read(h, rb.ctypes.data, len(rb), arr, lens, nb, sizes, 16, C.byref(n)))
+    assert n.value == 45
+    out = {"call": "wgcs_handle_virtio_read, one 65,535-B TSO read -> 45 segments, host buffers",
+           "median_us": round(gpu * 1e6, 1)}
+    if with_cpu:
+        import os
+        import sys
+
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+        import oracle  # cpu_baseline leg only
+
+        OL = oracle.lib()
+        cpu = timed(lambda: OL.or_handle_virtio_read(rb.ctypes.data, len(rb), arr, lens, nb, sizes, 16, C.byref(n)))
+        out["cpu_oracle_median_us"] = round(cpu * 1e6, 1)
+    return out
 
 
 def cpu_baseline(pkts, seconds, bytes_per_step):
