@@ -31,7 +31,7 @@ for k in range(40):
 torch.cuda.synchronize()
 buf = np.zeros(1 << 16, dtype=np.uint64)
 L.wgcs_exp_stamps(buf.ctypes.data, buf.nbytes)
-nw = n_jobs * 4 * 4
+nw = n_jobs * 2 * 16  # (job, segment group) blocks x 16 waves
 S = buf[: nw * 8].reshape(nw, 8).astype(np.int64)
 t0 = S[:, 0][S[:, 0] > 0].min()
 out = {}
@@ -40,7 +40,7 @@ for k in range(5):
     v = S[:, k]
     m = v > 0
     out[f"t{k}_from_start"] = {q: int(np.percentile(v[m] - t0, q)) for q in (0, 10, 50, 90, 100)} if m.any() else None
-for a, b in ((0, 1), (1, 2), (2, 3), (3, 4)):
+for a, b in ((0, 1), (1, 3), (3, 4), (0, 4), (0, 3)):
     m = (S[:, a] > 0) & (S[:, b] > 0)
     d = S[m, b] - S[m, a]
     out[f"d{a}{b}"] = {q: int(np.percentile(d, q)) for q in (10, 50, 90)} if m.any() else None
