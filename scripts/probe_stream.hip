@@ -79,3 +79,45 @@ extern "C" int probe_launch(const void* src, size_t bytes, void* out, int grid, 
   else { if (u == 2) L(2, false); else if (u == 4) L(4, false); else L(8, false); }
   return (int)hipGetLastError();
 }
+
+// Whole-wave-per-packet pattern with F packets in flight per wave: packet f's
+// chunk c = lane + 64u (u < 2: 2 KiB covers a 1500-B packet), so every load
+// instruction reads 1 KiB contiguous.
+template <int F>
+__global__ __launch_bounds__(256) void probe_wavef(const uint8_t* __restrict__ arena, uint32_t npk, uint32_t stride,
+                                                   uint32_t* __restrict__ out) {
+  const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t nw = gridDim.x * 4;
+  const int lane = threadIdx.x & 63;
+  uint32_t acc = 0;
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  for (uint32_t base = wave * F; base < npk; base += nw * F) {
+    u4 v[F][2];
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      const uint32_t p = base + f;
+      const uint8_t* pkt = arena + (size_t)p * stride;
+      const int rel0 = 12 - (int)(((uintptr_t)pkt + 12) & 15);
+      const int nch = p < npk ? ((int)stride - rel0 + 15) >> 4 : 0;
+      const u4* src = (const u4*)(pkt + rel0);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = lane + 64 * u;
+        v[f][u] = c < nch ? __builtin_nontemporal_load(src + c) : u4{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) acc += v[f][u].x + v[f][u].y + v[f][u].z + v[f][u].w;
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+extern "C" int probe_wavef_launch(const void* src, uint32_t npk, uint32_t stride, void* out, int grid, int f,
+                                  void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (f == 1) hipLaunchKernelGGL((probe_wavef<1>), dim3(grid), dim3(256), 0, s, (const uint8_t*)src, npk, stride, (uint32_t*)out);
+  else if (f == 2) hipLaunchKernelGGL((probe_wavef<2>), dim3(grid), dim3(256), 0, s, (const uint8_t*)src, npk, stride, (uint32_t*)out);
+  else hipLaunchKernelGGL((probe_wavef<4>), dim3(grid), dim3(256), 0, s, (const uint8_t*)src, npk, stride, (uint32_t*)out);
+  return (int)hipGetLastError();
+}

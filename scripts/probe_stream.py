@@ -44,5 +44,18 @@ for grid in (1024, 2048):
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / 100
         print(json.dumps({"pattern": "rows16x4 (checksum kernel access pattern)", "grid": grid, "nt": nt, "us": round(us, 2), "GBps": round(nbytes / us / 1e3, 1)}))
+L.probe_wavef_launch.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+for grid in (1024, 2048, 4096):
+    for f in (1, 2, 4):
+        for k in range(5):
+            L.probe_wavef_launch(bufs[k % R].data_ptr(), 65536, 1500, out.data_ptr(), grid, f, st.cuda_stream)
+        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for k in range(100):
+            L.probe_wavef_launch(bufs[k % R].data_ptr(), 65536, 1500, out.data_ptr(), grid, f, st.cuda_stream)
+        e1.record(st)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / 100
+        print(json.dumps({"pattern": f"wave-per-packet, {f} packets in flight (1 KiB per load instruction)", "grid": grid, "nt": 1, "us": round(us, 2), "GBps": round(nbytes / us / 1e3, 1)}))
 best = max(res)
 print(json.dumps({"best_GBps": round(best[0], 1), "frac_8TBs": round(best[0] / 8000, 3), "grid": best[1], "U": best[2], "nt": best[3]}))
