@@ -22,9 +22,9 @@ step() {
 }
 for s in "$@"; do
   case $s in
-    tests) step tests 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests) step tests 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     tests-all) step tests 1100 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
-    tests-gso) step tests_gso 600 python -m pytest tests/test_gpu_gso.py tests/test_golden.py -m gpu -q -p no:cacheprovider ;;
+    tests-gso) step tests_gso 600 python -u -m pytest tests/test_gpu_gso.py tests/test_gpu_stager.py tests/test_gpu_fullsize.py tests/test_golden.py -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     sweep) step sweep 400 python scripts/sweep_checksum.py ;;
     sweep-align) step sweep_align 400 python scripts/sweep_checksum.py --variants 16:6:8:1:16,16:6:8:1:64,16:6:8:1:128,16:8:8:1:16,16:8:8:1:64,16:8:8:1:128 ;;
     sweep-cfg3) step sweep_cfg3 400 python scripts/sweep_checksum.py --config cfg3 ;;

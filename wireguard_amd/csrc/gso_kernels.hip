@@ -7,10 +7,11 @@
 //
 // Mapping (gso_rows_kernel): one 16-lane DPP row per OUTPUT segment (slot =
 // job * max_segs + i), 64 segments per 1024-thread block, grid = (job,
-// segment group).  Wave 0 decodes the job once (validation, geometry and the
-// job-constant header sums) and broadcasts it through LDS; then every row
-//   1. issues its header-chunk loads (L2-resident, shared by the job) and its
-//      payload loads: dword-aligned 16-byte windows, U per lane in flight;
+// segment group).  Every row first issues its payload loads (dword-aligned
+// 16-byte windows, U per lane in flight), which need only gsoSize; wave 0
+// meanwhile decodes the job (validation, geometry and the job-constant header
+// sums) and broadcasts it through LDS; then every row
+//   1. issues its header-chunk loads (L2-resident, shared by the job);
 //   2. shifts each window to the destination's byte phase (alignbyte with the
 //      next lane's first dword via DPP row_ror), sums the L4 bytes from the
 //      same registers (v_dot2) and stores full global_store_dwordx4 chunks;
@@ -237,19 +238,18 @@ __device__ void none_segment(const uint8_t* rb, const Job& j, uint8_t* dst, int 
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// Row-per-segment split (default path): one 16-lane DPP row per OUTPUT
-// segment, 4 segments per wave, 16 per 256-thread block; grid = (job, group
-// of 16 segments).  Every wave decodes its job from L2-resident header bytes
-// (no separate plan launch).  Per row:
-//   * lanes r < hk fetch the segment's header chunk (two aligned 16-B loads +
-//     funnel to the destination phase) -- issued first, L2 hits;
-//   * the payload streams with U 16-byte non-temporal loads per lane in
-//     flight; destination chunk k = r + 16u is assembled from source chunks k
-//     and k+1 (k+1 comes from the next lane via DPP row_ror:15) and a per-row
-//     funnel shift, summed (v_dot2) and stored as one dwordx4;
-//   * header lanes patch the header (gro.go:1419-1465), add the IPv4 header,
-//     L4 header and pseudo-address bytes to the row sums, and after two row
-//     reductions store the header chunks with both checksums filled in.
+// Row-per-segment split: one 16-lane DPP row per OUTPUT segment, 64 rows per
+// 1024-thread block (wave 0 decodes the job once, LDS broadcast); grid =
+// (job, group of 64 segments).  Per row:
+//   * the first U payload windows are loaded speculatively (gsoSize only)
+//     before the decode finishes; further batches follow the decoded bounds;
+//   * the header source chunks are fetched after the barrier (L2 hits);
+//   * destination chunk k = r + 16u is assembled from the dword-aligned source
+//     window k and the next lane's first dword (DPP row_ror:15) with a per-row
+//     byte shift, summed (v_dot2) and stored as one dwordx4;
+//   * the checksums come from the row sum plus job constants plus the
+//     rewritten field values (gro.go:1419-1465), and the header chunks are
+//     stored last with both checksums filled in.
 // Each output byte is written exactly once, each input byte read once.
 
 // DPP row_ror:15 -- lane r of each 16-lane row receives lane (r + 1) & 15.
@@ -446,6 +446,7 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   const uint32_t jb = blockIdx.x;
   GSO_STAMP(0);
   const uint8_t* vb = arena + jobs[jb].off;
+  const uint32_t jlen = jobs[jb].len;
   const uint8_t* rb = vb + 10;
   const uint64_t slot0 = (uint64_t)jb * max_segs;  // sizes[] index of segment 0
   // segment i of this job at out + obase + i * opitch (+ offset): fixed slots,
@@ -456,9 +457,18 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
     obase = outpos[jb].base;
     opitch = outpos[jb].pitch;
   }
+  const uint32_t seg0 = blockIdx.y * 64u + (uint32_t)wv * 4u;  // wave-uniform
+  const int i = (int)seg0 + (lane >> 4);                       // this row's segment
+  uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
+  const int dalign = (int)((uintptr_t)dst & 15u);
+  uint8_t* dbase = dst - dalign;
+
+  // ---- wave 0: decode the job (validation, geometry, job-constant header
+  // sums) and publish it through LDS.  It runs before wave 0's own
+  // speculative loads: a decode step that waited on a global load would
+  // otherwise wait (vmcnt retires in order) for that whole payload batch.
+  HdrBytes hb;
   if (wv == 0) {
-    const uint32_t jlen = jobs[jb].len;
-    HdrBytes hb;
     hb.load(vb, (int)min(jlen, 256u), lane);
     const Job j = decode_job(hb, jlen, jobs[jb].flags, room, max_segs);
     const bool ok = j.status == 0 || j.status == WGCS_ERR_TOO_MANY_SEGMENTS;
@@ -494,13 +504,49 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
       }
     }
   }
+
+  // ---- speculative first payload batch.  The source window of segment i
+  // needs only gsoSize (virtio header bytes 4-5), so every row issues its
+  // first U payload loads before the block barrier: the decode and the
+  // barrier overlap the HBM round trip instead of preceding it.  The
+  // guards keep the loads inside the job's own bytes [vb, rb + plen); bytes a
+  // window picks up outside the segment are masked exactly as on the decoded
+  // path (header positions, past pktLen).  GSO_NONE jobs skip it.
+  int gso_s = 0, type_s = GSO_NONE;
+  if (wv == 0) {
+    if (jlen >= 10) {
+      type_s = (int)hb(1);
+      gso_s = (int)hb.le16(4);
+    }
+  } else if (jlen >= 10) {
+    type_s = (int)u8at(vb + 1);
+    gso_s = (int)(u8at(vb + 4) | (u8at(vb + 5) << 8));
+  }
+  const int plen_s = jlen >= 10 ? (int)jlen - 10 : 0;
+  const uint8_t* jend = rb + plen_s;
+  const uint8_t* w0 = rb + (int64_t)i * gso_s - dalign;  // source of destination chunk 0 (payload positions)
+  const int sb = (int)((uintptr_t)w0 & 3u);              // byte shift within dwords
+  const uint8_t* abase = w0 - sb;                        // dword-aligned window base
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  uint4 A[U];
+  uint32_t E = 0;
+  const bool spec = type_s != GSO_NONE && (int64_t)i * gso_s < (int64_t)plen_s;  // row-uniform
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint8_t* ca = abase + 16 * (r + 16 * u);
+    A[u] = (spec && ca >= vb && ca < jend) ? ld_window<NT>(ca, jend) : z;
+  }
+  if (spec && r == 15) {
+    const uint8_t* ce = abase + 16 * (16 * U);
+    if (ce >= vb && ce < jend) E = *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(ce, 4));
+  }
+
   __syncthreads();
   GSO_STAMP(1);
   Job j = {};
   j.status = ufl(ji.status);
   j.nseg = ufl(ji.nseg);
   j.type = ufl(ji.type);
-  const uint32_t seg0 = blockIdx.y * 64u + (uint32_t)wv * 4u;  // wave-uniform
   if (j.nseg == 0) return;  // error status (or an empty packet)
   j.plen = ufl(ji.plen);
   j.cs = ufl(ji.cs);
@@ -522,8 +568,8 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   const uint32_t ip_base = (uint32_t)ufl((int)ji.ip_base), l4_base = (uint32_t)ufl((int)ji.l4_base);
   const uint32_t addr_sum = (uint32_t)ufl((int)ji.addr), tflags = (uint32_t)ufl((int)ji.tflags);
   const bool v4 = j.ipv == 4, tcp = j.type != GSO_UDP_L4;
-  const int i = (int)seg0 + (lane >> 4);
   if (i >= j.nseg) return;  // whole rows retire; DPP below stays inside live rows
+  const bool spec_ok = spec && j.gso == gso_s;  // always true: both read virtio bytes 4-5
 
   // ---- segment geometry (row-uniform)
   const int hdr_len = j.hdr_len, cs = j.cs, plen = j.plen;
@@ -534,17 +580,10 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   const int pkt_len = hdr_len + seg_len;
   const bool last = seg_end == plen;
   const uint64_t slot = slot0 + (uint32_t)i;
-  uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
-  const int dalign = (int)((uintptr_t)dst & 15u);
-  uint8_t* dbase = dst - dalign;
   const int nk = (pkt_len + dalign + 15) >> 4;
   const int hk = min((hdr_len + dalign + 15) >> 4, nk);
-  const uint8_t* w0 = rb + i * j.gso - dalign;  // source of destination chunk 0 (payload positions)
-  const int sb = (int)((uintptr_t)w0 & 3u);     // byte shift within dwords
-  const uint8_t* abase = w0 - sb;               // dword-aligned window base
   const uint8_t* src_lo = rb + seg_start;
   const uint8_t* src_hi = rb + seg_end;
-  const uint4 z = make_uint4(0, 0, 0, 0);
 
   // ---- header source loads first (shared by the job's segments: L2 hits).
   // fast: packet coordinates (lane r = readBuf[16r, 16r + 16), wave-uniform
@@ -563,16 +602,17 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   uint32_t acc = 0;  // L4 bytes [hdrLen, pktLen): LE words at destination addresses
   uint4 keep = z;    // payload part of header chunk r (r < hk)
   for (int k0 = 0; k0 < nk; k0 += 16 * U) {
-    uint4 A[U];
+    if (k0 > 0 || !spec_ok) {  // wave-uniform; the first batch is normally the speculative one
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint8_t* ca = abase + 16 * (k0 + r + 16 * u);
-      A[u] = (ca < src_hi && ca + 16 > src_lo) ? ld_window<NT>(ca, src_hi) : z;
-    }
-    uint32_t E = 0;
-    if (r == 15) {
-      const uint8_t* ce = abase + 16 * (k0 + 16 * U);
-      if (ce < src_hi && ce + 4 > src_lo) E = *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(ce, 4));
+      for (int u = 0; u < U; ++u) {
+        const uint8_t* ca = abase + 16 * (k0 + r + 16 * u);
+        A[u] = (ca < src_hi && ca + 16 > src_lo) ? ld_window<NT>(ca, src_hi) : z;
+      }
+      E = 0;
+      if (r == 15) {
+        const uint8_t* ce = abase + 16 * (k0 + 16 * U);
+        if (ce < src_hi && ce + 4 > src_lo) E = *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(ce, 4));
+      }
     }
     uint32_t Rc = row_next(A[0].x);  // lane 15: lane 0's next-u dword
 #pragma unroll
