@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS) + ["cfg4", "gro"])
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS) + ["cfg4", "gro", "udp_split", "udp_coalesce"])
     ap.add_argument("--mode", default="validate", choices=["validate", "fill"])
     ap.add_argument("--rotate", type=int, default=4, help="distinct batch copies (defeat the 256 MiB MALL)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
@@ -90,6 +90,10 @@ def main():
         from wireguard_amd import gro_bench
 
         return gro_bench.run(args, torch, dev, dist, rank, world, local, barrier)
+    if args.config in ("udp_split", "udp_coalesce"):
+        from wireguard_amd import udp_bench
+
+        return udp_bench.run(args, torch, dev, dist, rank, world, local, barrier)
 
     n_cfg, flen, kinds, cfg_idx, scaling = CONFIGS[args.config]
     mode = MODE_VALIDATE if args.mode == "validate" else MODE_L4_FILL

@@ -22,6 +22,12 @@
  *   wgcs_handle_virtio_read   handleVirtioRead(readBuf, bufs, sizes, offset)  tun/tun.go:514-632
  *   wgcs_handle_gro           handleGRO(bufs, offset, tcpTable, udpTable, canUDPGRO, &toWrite)
  *                                                                 tun/gro.go:1326-1367
+ *   wgcs_get_gso_size         getGSOSize(control)                 conn/gso.go:35-67
+ *   wgcs_set_gso_size         setGSOSize(&control, gsoSize)       conn/gso.go:71-100
+ *   wgcs_split_messages       splitMessages(msgs, firstMsgAt)     conn/bind.go:542-597
+ *   wgcs_split_messages_batch device-resident batch of splitMessages calls (one per recvmmsg)
+ *   wgcs_coalesce_messages    coalesceMessages(msgs, bufs, ep, addr)  conn/bind.go:599-662
+ *   wgcs_coalesce_messages_batch  device-resident batch of coalesceMessages calls (one per Send)
  * Status codes map 1:1 onto the reference's Go errors (see WGCS_ERR_*).
  */
 #ifndef WGCSUM_H
@@ -53,6 +59,8 @@ extern "C" {
 #define WGCS_ERR_OUT_OF_RANGE (-13)     /* input on which the Go code would panic (slice bounds) */
 #define WGCS_ERR_BATCH_FULL (-14)       /* stager: the open batch has no room; submit it first */
 #define WGCS_ERR_NOT_READY (-15)        /* stager: batch id not submitted / recycled */
+#define WGCS_ERR_CMSG (-16)             /* "error parsing socket control message: %w" conn/gso.go:45 */
+#define WGCS_ERR_SPLIT_OVERFLOW (-17)   /* "splitting coalesced packet resulted in overflow" conn/bind.go:565 */
 #define WGCS_ERR_HIP (-100)             /* HIP runtime error (message: wgcs_last_error) */
 #define WGCS_ERR_NOMEM (-101)
 #define WGCS_ERR_NO_DEVICE (-102)
@@ -199,6 +207,69 @@ int wgcs_stager_result(wgcs_stager *st, uint64_t batch, int read_idx, int *statu
  * leaves them (sizes[], n, ErrTooManySegments / slice-bound checks) */
 int wgcs_stager_copy_out(wgcs_stager *st, uint64_t batch, int read_idx, uint8_t *const *bufs,
                          const size_t *buf_lens, int nbufs, int *sizes, int offset, int *n_out);
+
+/* ---- outer-UDP message batching (conn/bind.go, conn/gso.go) ----
+ * The UDP side of the same batch loop: recvmmsg with UDP_GRO hands back up to
+ * BatchSize/64 coalesced datagrams that splitMessages cuts into packets, and
+ * Send coalesces runs of equal-size packets for UDP_SEGMENT (conn/bind.go:25-36:
+ * maxIPv4PayloadLen 65507, maxIPv6PayloadLen 65527, maxUDPSegments 64). */
+
+/* getGSOSize(msg.OOB[:msg.NN]): the UDP_GRO size (0 if absent) or WGCS_ERR_CMSG */
+int wgcs_get_gso_size(const uint8_t *control, size_t len, int *gso_size);
+/* setGSOSize(&control, gsoSize): appends a SOL_UDP/UDP_SEGMENT cmsg (24 bytes)
+ * when it fits in cap; *len is len(control) in and out */
+int wgcs_set_gso_size(uint8_t *control, size_t *len, size_t cap, uint16_t gso_size);
+
+/* splitMessages over n_batches recvmmsg batches of n_msgs messages each.
+ * Message slot q = b*n_msgs + s.  Input: the recvmmsg landing buffers only --
+ * msgs[s].Buffers[0] for s >= first_msg_at (buf_len bytes, len == cap) at
+ * d_in + (b*(n_msgs - first_msg_at) + s - first_msg_at)*in_stride;
+ * d_n_in[q] = msgs[s].N (all s), d_gso[q] = getGSOSize result (>= 0) or WGCS_ERR_CMSG.
+ * Output, out of place: packet k of batch b at d_out + (b*n_msgs + k)*out_stride
+ * (16-byte aligned, out_stride >= the largest packet), d_n_out[q] = the final
+ * msgs[s].N (packet length, 0 for a source zeroed by :589-594, else unchanged),
+ * d_src[q] = index s' whose Addr the slot now carries (:570) or -1 if unchanged;
+ * d_count[b] = nPackets, d_status[b] = 0 / WGCS_ERR_CMSG / WGCS_ERR_SPLIT_OVERFLOW /
+ * WGCS_ERR_OUT_OF_RANGE (Buffers[0][0:gsoSize] beyond cap) / WGCS_ERR_INVALID_ARG
+ * (N > buf_len or a packet larger than out_stride).  On an error status the
+ * packets before it are written, as the reference copies them before returning. */
+int wgcs_split_messages_batch(wgcs_ctx *ctx, const uint8_t *d_in, uint64_t in_stride, uint32_t buf_len,
+                              const int32_t *d_n_in, const int32_t *d_gso, uint32_t n_msgs,
+                              uint32_t first_msg_at, uint32_t n_batches, uint8_t *d_out,
+                              uint64_t out_stride, int32_t *d_n_out, int32_t *d_src, int32_t *d_count,
+                              int32_t *d_status, void *stream);
+
+/* coalesceMessages over n_batches Send batches, in place.  Batch b has
+ * d_nbufs[b] <= max_bufs buffers; buffer j is slot q = b*max_bufs + j at
+ * d_bufs + q*buf_stride (16-byte aligned), len(bufs[j]) = d_lens[q],
+ * cap(bufs[j]) = min(d_caps[q], buf_cap) (d_caps NULL: buf_cap; buf_cap <= buf_stride).
+ * Appends land in the first buffer of each run, as Go's append within cap does.
+ * Per batch: d_n_msgs[b] = nMsgs; per message m (index b*max_bufs + m):
+ * d_msg_first = the buffer j that msgs[m].Buffers[0] aliases, d_msg_len = its
+ * final length, d_msg_gso = the UDP_SEGMENT size set by setGSOSize, or -1 if none. */
+int wgcs_coalesce_messages_batch(wgcs_ctx *ctx, uint8_t *d_bufs, uint64_t buf_stride, uint32_t buf_cap,
+                                 const int32_t *d_caps, const int32_t *d_lens, const int32_t *d_nbufs,
+                                 uint32_t max_bufs, uint32_t n_batches, int dst_is_v6, int32_t *d_n_msgs,
+                                 int32_t *d_msg_first, int32_t *d_msg_len, int32_t *d_msg_gso,
+                                 void *stream);
+
+/* splitMessages(msgs, firstMsgAt) on host buffers: bufs[i] = msgs[i].Buffers[0]
+ * (buf_len bytes each, len == cap, as device/receive.go:119 passes them),
+ * ns[i] = msgs[i].N (in/out), oobs[i][0:nns[i]] = msgs[i].OOB[:msgs[i].NN];
+ * addr_src[i] = the message whose Addr msgs[i] carries afterwards (i if unchanged).
+ * Returns the status, *n_packets = nPackets. */
+int wgcs_split_messages(wgcs_ctx *ctx, uint8_t *const *bufs, size_t buf_len, int *ns,
+                        const uint8_t *const *oobs, const size_t *nns, int n_msgs, int first_msg_at,
+                        int *addr_src, int *n_packets);
+/* coalesceMessages(msgs, bufs, endpoint, addr) on host buffers (len/cap per
+ * buffer, len <= 65536): appends into bufs[msg_first[m]] within its capacity;
+ * msg_len[m] = len(msgs[m].Buffers[0]).  oobs (optional, m < nbufs): msgs[m].OOB
+ * with oob_lens in/out and oob_caps -- setSrcControl(src_ctl) then setGSOSize
+ * for runs of > 1 packet, as conn/bind.go:634,647,657 do.  *n_msgs = nMsgs. */
+int wgcs_coalesce_messages(wgcs_ctx *ctx, uint8_t *const *bufs, const size_t *lens, const size_t *caps,
+                           int nbufs, int dst_is_v6, const uint8_t *src_ctl, size_t src_len,
+                           uint8_t *const *oobs, size_t *oob_lens, const size_t *oob_caps,
+                           int *msg_first, size_t *msg_len, int *n_msgs);
 
 #ifdef __cplusplus
 }

@@ -163,3 +163,87 @@ def closed_form_checksum(b: bytes, initial: int = 0) -> int:
         b += b"\0"
     s = int(np.frombuffer(b, dtype=">u2").astype(np.uint64).sum()) + initial
     return 0 if s == 0 else 1 + (s - 1) % 0xFFFF
+
+
+# ---------------------------------------------------------------------------
+# Outer-UDP message batching (conn/bind.go:542-662, conn/gso.go:35-100),
+# wg_oracle_conn.c.  Messages are duck-typed: .buf (numpy uint8, cap = len),
+# .buf_len, .n, .oob (numpy uint8, cap = len), .oob_len, .nn, .addr.
+# ---------------------------------------------------------------------------
+class _OrMsg(C.Structure):
+    _fields_ = [("buf", C.c_void_p), ("buf_len", C.c_size_t), ("buf_cap", C.c_size_t), ("n", C.c_int),
+                ("oob", C.c_void_p), ("oob_len", C.c_size_t), ("oob_cap", C.c_size_t), ("nn", C.c_int),
+                ("addr", C.c_int)]
+
+
+def _conn_lib():
+    L = lib()
+    if not getattr(L, "_conn_ready", False):
+        L.or_get_gso_size.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_int)]
+        L.or_get_gso_size.restype = C.c_int
+        L.or_set_gso_size.argtypes = [C.c_void_p, C.POINTER(C.c_size_t), C.c_size_t, C.c_uint16]
+        L.or_set_gso_size.restype = None
+        L.or_split_messages.argtypes = [C.POINTER(_OrMsg), C.c_int, C.c_int, C.POINTER(C.c_int)]
+        L.or_split_messages.restype = C.c_int
+        L.or_coalesce_messages.argtypes = [C.POINTER(_OrMsg), C.c_int, C.POINTER(C.c_void_p),
+                                           C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.c_int, C.c_int,
+                                           C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_int)]
+        L.or_coalesce_messages.restype = C.c_int
+        L._conn_ready = True
+    return L
+
+
+def get_gso_size(control: bytes):
+    """getGSOSize -> (gso, rc)."""
+    a = np.frombuffer(bytes(control) + b"\0", dtype=np.uint8)
+    g = C.c_int(0)
+    rc = _conn_lib().or_get_gso_size(_ptr(a), len(control), C.byref(g))
+    return g.value, rc
+
+
+def set_gso_size(oob: np.ndarray, oob_len: int, gso: int) -> int:
+    """setGSOSize on oob[:oob_len] (cap len(oob)); returns the new length."""
+    ln = C.c_size_t(oob_len)
+    _conn_lib().or_set_gso_size(_ptr(oob), C.byref(ln), len(oob), gso & 0xFFFF)
+    return ln.value
+
+
+def split_messages(msgs: list, first_msg_at: int):
+    """splitMessages(msgs, firstMsgAt) -> (n_packets, rc); mutates msgs (addr
+    becomes the Addr of the source message, as an index into the original addrs)."""
+    n = len(msgs)
+    arr = (_OrMsg * n)()
+    for i, m in enumerate(msgs):
+        arr[i] = _OrMsg(m.buf.ctypes.data, len(m.buf), len(m.buf), m.n, m.oob.ctypes.data, m.oob_len,
+                        len(m.oob), m.nn, i)
+    npk = C.c_int(0)
+    rc = _conn_lib().or_split_messages(arr, n, first_msg_at, C.byref(npk))
+    addrs = [m.addr for m in msgs]
+    for i, m in enumerate(msgs):
+        m.n = arr[i].n
+        m.addr = addrs[arr[i].addr]
+    return npk.value, rc
+
+
+def coalesce_messages(msgs: list, bufs: list, lens: list, src_control: bytes, addr, dst_is_v6: bool):
+    """coalesceMessages -> n_msgs; msgs[m].buf aliases the run's first buffer,
+    msgs[m].buf_len its new length, msgs[m].oob/oob_len set as the reference does."""
+    nb = len(bufs)
+    arr = (_OrMsg * len(msgs))()
+    for i, m in enumerate(msgs):
+        arr[i] = _OrMsg(None, 0, 0, m.n, m.oob.ctypes.data, m.oob_len, len(m.oob), m.nn, -1)
+    cb = (C.c_void_p * max(nb, 1))(*[b.ctypes.data for b in bufs])
+    cl = (C.c_size_t * max(nb, 1))(*lens)
+    cc = (C.c_size_t * max(nb, 1))(*[len(b) for b in bufs])
+    sc = np.frombuffer(bytes(src_control) + b"\0", dtype=np.uint8)
+    nm = C.c_int(0)
+    rc = _conn_lib().or_coalesce_messages(arr, len(msgs), cb, cl, cc, nb, int(dst_is_v6), _ptr(sc),
+                                          len(src_control), 0, C.byref(nm))
+    assert rc == 0, rc
+    index = {b.ctypes.data: j for j, b in enumerate(bufs)}
+    for m in range(nm.value):
+        msgs[m].buf = bufs[index[arr[m].buf]]
+        msgs[m].buf_len = arr[m].buf_len
+        msgs[m].oob_len = arr[m].oob_len
+        msgs[m].addr = addr
+    return nm.value

@@ -42,6 +42,13 @@ extern "C" {
 #define OR_ERR_CSUM_OFFSET (-11)
 #define OR_ERR_READ_OVERFLOW (-12)
 #define OR_ERR_OUT_OF_RANGE (-13) /* reference would panic (slice out of range) */
+#define OR_ERR_CMSG (-16)           /* "error parsing socket control message: %w"  conn/gso.go:45 */
+#define OR_ERR_SPLIT_OVERFLOW (-17) /* "splitting coalesced packet resulted in overflow" conn/bind.go:565 */
+
+/* conn/bind.go:25-36 */
+#define OR_MAX_IPV4_PAYLOAD ((1 << 16) - 1 - 20 - 8)
+#define OR_MAX_IPV6_PAYLOAD ((1 << 16) - 1 - 8)
+#define OR_MAX_UDP_SEGMENTS 64
 
 typedef struct or_virtio_hdr {
   uint8_t flags;
@@ -97,6 +104,35 @@ void or_checksum_batch(int mode, uint8_t *arena, const or_pkt *pkts,
 /* Multithreaded VALIDATE/L4_FILL batch for the CPU baseline (pthreads). */
 void or_checksum_batch_mt(int mode, uint8_t *arena, const or_pkt *pkts,
                           uint32_t n, void *out, int threads);
+
+/* ---- outer-UDP message batching (conn/bind.go, conn/gso.go; wg_oracle_conn.c) ---- */
+/* one ipv6.Message: Buffers[0] (len/cap), N, OOB (len/cap), NN, Addr (opaque id) */
+typedef struct or_msg {
+  uint8_t *buf;
+  size_t buf_len, buf_cap;
+  int n;
+  uint8_t *oob;
+  size_t oob_len, oob_cap;
+  int nn;
+  int addr;
+} or_msg;
+/* conn/gso.go:35-67 */
+int or_get_gso_size(const uint8_t *control, size_t len, int *gso);
+/* conn/gso.go:71-100 */
+void or_set_gso_size(uint8_t *control, size_t *len, size_t cap, uint16_t gso);
+/* conn/sticky.go:101-107 */
+void or_set_src_control(uint8_t *control, size_t *len, size_t cap, const uint8_t *src, size_t src_len);
+/* conn/bind.go:542-597 */
+int or_split_messages(or_msg *msgs, int n_msgs, int first_msg_at, int *n_packets);
+/* conn/bind.go:599-662 */
+int or_coalesce_messages(or_msg *msgs, int n_msgs_cap, uint8_t *const *bufs, const size_t *lens,
+                         const size_t *caps, int nbufs, int dst_is_v6, const uint8_t *src_ctl,
+                         size_t src_len, int addr, int *n_msgs);
+/* batch drivers (tests, cpu_baseline): slot q = b*n + s at base + q*stride */
+void or_split_batch(uint8_t *bufs, size_t stride, size_t buf_len, int *ns, uint8_t *oobs, size_t oob_stride,
+                    const int *nns, int n_msgs, int first, int n_batches, int *counts, int *statuses);
+void or_coalesce_batch(uint8_t *bufs, size_t stride, const size_t *lens, const size_t *caps, const int *nbufs,
+                       int max_bufs, int n_batches, int dst_is_v6, int *n_msgs_out);
 
 #ifdef __cplusplus
 }

@@ -25,6 +25,10 @@ for s in "$@"; do
     tests) step tests 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     tests-all) step tests 1100 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     tests-gso) step tests_gso 600 python -u -m pytest tests/test_gpu_gso.py tests/test_gpu_stager.py tests/test_gpu_fullsize.py tests/test_golden.py -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    tests-conn) step tests_conn 400 python -u -m pytest tests/test_gpu_conn.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    bench-usplit) step bench_usplit 300 python bench.py --config udp_split --steps 100 --warmup 10 --cpu-seconds 5 ;;
+    bench-ucoal) step bench_ucoal 300 python bench.py --config udp_coalesce --steps 100 --warmup 10 --cpu-seconds 5 ;;
+    prof-udp) (cd /tmp && step prof_usplit 300 rocprofv3 --kernel-trace --stats -d "$OUT/profusplit_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config udp_split --steps 50 --warmup 5 --cpu-seconds 0) && (cd /tmp && step prof_ucoal 300 rocprofv3 --kernel-trace --stats -d "$OUT/profucoal_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config udp_coalesce --steps 50 --warmup 5 --cpu-seconds 0) ;;
     sweep) step sweep 400 python scripts/sweep_checksum.py ;;
     sweep-align) step sweep_align 400 python scripts/sweep_checksum.py --variants 16:6:8:1:16,16:6:8:1:64,16:6:8:1:128,16:8:8:1:16,16:8:8:1:64,16:8:8:1:128 ;;
     sweep-cfg3) step sweep_cfg3 400 python scripts/sweep_checksum.py --config cfg3 ;;

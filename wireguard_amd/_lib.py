@@ -31,6 +31,8 @@ ERR_READ_OVERFLOW = -12
 ERR_OUT_OF_RANGE = -13
 ERR_BATCH_FULL = -14
 ERR_NOT_READY = -15
+ERR_CMSG = -16
+ERR_SPLIT_OVERFLOW = -17
 ERR_HIP = -100
 ERR_NOMEM = -101
 ERR_NO_DEVICE = -102
@@ -106,6 +108,14 @@ def load() -> C.CDLL:
         "wgcs_stager_submit": ([vp, C.POINTER(u64)], i32),
         "wgcs_stager_wait": ([vp, u64], i32),
         "wgcs_stager_result": ([vp, u64, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(vp), C.POINTER(vp)], i32),
+        "wgcs_get_gso_size": ([vp, sz, C.POINTER(i32)], i32),
+        "wgcs_set_gso_size": ([vp, C.POINTER(sz), sz, C.c_uint16], i32),
+        "wgcs_split_messages_batch": ([vp, vp, u64, u32, vp, vp, u32, u32, u32, vp, u64, vp, vp, vp, vp, vp], i32),
+        "wgcs_coalesce_messages_batch": ([vp, vp, u64, u32, vp, vp, vp, u32, u32, i32, vp, vp, vp, vp, vp], i32),
+        "wgcs_split_messages": ([vp, u8pp, sz, C.POINTER(i32), u8pp, C.POINTER(sz), i32, i32, C.POINTER(i32),
+                                 C.POINTER(i32)], i32),
+        "wgcs_coalesce_messages": ([vp, u8pp, C.POINTER(sz), C.POINTER(sz), i32, i32, vp, sz, u8pp, C.POINTER(sz),
+                                    C.POINTER(sz), C.POINTER(i32), C.POINTER(sz), C.POINTER(i32)], i32),
         "wgcs_stager_copy_out": ([vp, u64, i32, u8pp, C.POINTER(sz), i32, C.POINTER(i32), i32, C.POINTER(i32)], i32),
     }
     for name, (args, res) in sig.items():

@@ -74,4 +74,14 @@ enum : uint8_t { GRO_KIND_V6 = 1, GRO_KIND_UDP = 2, GRO_KIND_PSH = 4 };
 hipError_t launch_gro_coalesce(const uint8_t* stage, const GroItem* items, uint32_t n_items, const GroSeg* segs,
                                uint32_t n_segs, uint8_t* out, hipStream_t s);
 
+// Outer-UDP message batching (conn/bind.go:542-662), udp_msgs_kernels.hip.
+hipError_t launch_udp_split(const uint8_t* in, uint64_t in_stride, uint32_t buf_len, const int32_t* n_in,
+                            const int32_t* gso, uint32_t n_msgs, uint32_t first, uint32_t n_batches, uint8_t* out,
+                            uint64_t out_stride, int32_t* n_out, int32_t* src, int32_t* count, int32_t* status,
+                            hipStream_t s);
+hipError_t launch_udp_coalesce(uint8_t* bufs, uint64_t stride, uint32_t buf_cap, const int32_t* caps,
+                               const int32_t* lens, const int32_t* nbufs, uint32_t max_bufs, uint32_t n_batches,
+                               int dst_is_v6, int32_t* n_msgs, int32_t* msg_first, int32_t* msg_len,
+                               int32_t* msg_gso, hipStream_t s);
+
 }  // namespace wgcs

@@ -1,0 +1,343 @@
+"""Outer-UDP message batching measurement: device-resident
+splitMessages / coalesceMessages (conn/bind.go:542-662) on one MI355X.
+Called by bench.py --config udp_split | udp_coalesce.
+
+udp_split:    1024 recvmmsg batches; each has the receive path's shape
+              (BatchSize 128, readAt 126, conn/bind.go:293): two UDP_GRO
+              datagrams of 45 x 1452-B WireGuard transport messages (MTU-1420
+              tunnel + 32 B of header/tag) -> 90 packets per batch.
+udp_coalesce: 1024 Send batches of 128 x 1452-B transport messages (IPv4
+              peer) -> runs of 45 / 45 / 38 appended into 3 messages.
+Algorithmic bytes per launch = payload bytes read + written (each packet byte
+moves once: the first buffer of a coalesced run stays where it is).
+"""
+from __future__ import annotations
+
+import json
+import time
+
+import numpy as np
+
+from . import synth
+
+HBM_PEAK_GBS = 8000.0
+MSG = 1452  # transport message for a 1420-B tunnel MTU: 16-B header + 1420 + 16-B tag
+SEGS = 45  # 45 * 1452 = 65340 <= maxIPv4PayloadLen 65507 < 46 * 1452
+
+
+def _oracle():
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import oracle  # cpu_baseline / host-call comparison only
+
+    return oracle
+
+
+def _gro_cmsg(g):
+    return (18).to_bytes(8, "little") + (17).to_bytes(4, "little") + (104).to_bytes(4, "little") + \
+        int(g).to_bytes(2, "little") + bytes(6)
+
+
+def _time_steps(torch, stream, step, steps, warmup, barrier):
+    for k in range(warmup):
+        step(k)
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for k in range(steps):
+        step(warmup + k)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    return time.perf_counter() - t0, e0.elapsed_time(e1) / steps
+
+
+def _copy_ms(torch, stream, dst, src, nbytes, steps):
+    """Calibration: the runtime's device copy kernel moving the same bytes."""
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            dst[:nbytes].copy_(src[:nbytes])
+        c0 = torch.cuda.Event(enable_timing=True)
+        c1 = torch.cuda.Event(enable_timing=True)
+        c0.record(stream)
+        for _ in range(steps):
+            dst[:nbytes].copy_(src[:nbytes])
+        c1.record(stream)
+    torch.cuda.synchronize()
+    return c0.elapsed_time(c1) / steps
+
+
+def run(args, torch, dev, dist, rank, world, local, barrier):
+    if args.config == "udp_split":
+        res = run_split(args, torch, dev, rank, world, barrier)
+    else:
+        res = run_coalesce(args, torch, dev, rank, world, barrier)
+    if dist is not None:
+        t = torch.tensor([res.pop("_elapsed")], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    else:
+        elapsed = res.pop("_elapsed")
+    bps = res["roofline"]["algorithmic_bytes_per_launch"]
+    res["value"] = round(bps * args.steps * world / elapsed / 2**30, 2)
+    res["ms_per_step"] = round(elapsed / args.steps * 1e3, 5)
+    res["n_gpus"] = world
+    res["config"]["parallelism"] = f"shard{world} (no collective)"
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    dev.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _result(metric, args, workload, extra, kname, kern_ms, bps, copy_ms, elapsed):
+    achieved = bps / (kern_ms * 1e-3) / 1e9
+    return {
+        "metric": metric, "value": None, "unit": "GiB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic", "config": {"workload": workload, **extra},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
+                     "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_launch": bps,
+                     "d2d_copy_same_bytes_ms": round(copy_ms, 5)},
+        "_elapsed": elapsed,
+    }
+
+
+# --------------------------------------------------------------------- split
+def run_split(args, torch, dev, rank, world, barrier, B=1024, n_msgs=128, first=126):
+    ns = n_msgs - first
+    rng = np.random.default_rng(synth.SEED + 77 + rank)
+    in_stride, out_stride, buf_len = 65536, 1456, 65535
+    R = 2
+    srcs = rng.integers(0, 256, (B * ns, SEGS * MSG), dtype=np.uint8)
+    n_in = np.zeros(B * n_msgs, np.int32)
+    gso = np.zeros(B * n_msgs, np.int32)
+    for b in range(B):
+        n_in[b * n_msgs + first: (b + 1) * n_msgs] = SEGS * MSG
+        gso[b * n_msgs + first: (b + 1) * n_msgs] = MSG
+    stream = torch.cuda.Stream()
+    d_in = []
+    for _ in range(R):
+        t = torch.zeros((B * ns, in_stride), dtype=torch.uint8, device="cuda")
+        t[:, : SEGS * MSG].copy_(torch.from_numpy(srcs))
+        d_in.append(t)
+    d_n, d_g = torch.from_numpy(n_in).cuda(), torch.from_numpy(gso).cuda()
+    d_out = [torch.empty((B * n_msgs, out_stride), dtype=torch.uint8, device="cuda") for _ in range(R)]
+    d_nout = torch.zeros(B * n_msgs, dtype=torch.int32, device="cuda")
+    d_src = torch.zeros(B * n_msgs, dtype=torch.int32, device="cuda")
+    d_cnt = torch.zeros(B, dtype=torch.int32, device="cuda")
+    d_st = torch.zeros(B, dtype=torch.int32, device="cuda")
+    L, h, s = dev.lib, dev.h, stream.cuda_stream
+
+    def step(k):
+        i = k % R
+        rc = L.wgcs_split_messages_batch(h, d_in[i].data_ptr(), in_stride, buf_len, d_n.data_ptr(), d_g.data_ptr(),
+                                         n_msgs, first, B, d_out[i].data_ptr(), out_stride, d_nout.data_ptr(),
+                                         d_src.data_ptr(), d_cnt.data_ptr(), d_st.data_ptr(), s)
+        assert rc == 0
+
+    elapsed, kern_ms = _time_steps(torch, stream, step, args.steps, args.warmup, barrier)
+    cnt, st = d_cnt.cpu().numpy(), d_st.cpu().numpy()
+    assert (st == 0).all() and (cnt == ns * SEGS).all(), (st[:4], cnt[:4])
+    # size-independent property: packet k of batch b is bytes [k*1452, +1452) of its datagram
+    out = d_out[0].view(B, n_msgs, out_stride)
+    for b in (0, B // 2, B - 1):
+        got = out[b, : ns * SEGS, :MSG].cpu().numpy().reshape(-1)
+        assert np.array_equal(got, srcs[b * ns:(b + 1) * ns].reshape(-1)), b
+    payload = B * ns * SEGS * MSG
+    bps = 2 * payload
+    copy_ms = _copy_ms(torch, stream, d_out[0].view(-1), d_in[0].view(-1), payload, args.steps)
+    res = _result("device-resident UDP GRO split GiB/s (bytes read + written), 1024 recvmmsg batches x 2 x 45 x 1452 B",
+                  args, f"{B} recvmmsg batches (BatchSize {n_msgs}, readAt {first}): {ns} UDP_GRO datagrams of "
+                  f"{SEGS} x {MSG}-B transport messages each -> {ns * SEGS} packets per batch; splitMessages, "
+                  "conn/bind.go:542-597 (SURVEY.md §8f row 3)",
+                  {"batches": B, "packets_per_step": B * ns * SEGS, "payload_bytes": payload, "rotated_copies": R},
+                  "udp_split_kernel<6>", kern_ms, bps, copy_ms, elapsed)
+    if rank == 0 and world == 1:
+        res["host_call"] = split_host_call(dev, with_cpu=args.cpu_seconds > 0)
+        if args.cpu_seconds > 0:
+            res["cpu_baseline"] = split_cpu_baseline(srcs, args.cpu_seconds)
+    return res
+
+
+def split_host_call(dev, with_cpu: bool, reps: int = 200):
+    """Latency of one reference-shaped splitMessages call (wgcs_split_messages:
+    128 host buffers, 2 GRO datagrams at 126/127) -- one C call, prebuilt args."""
+    import ctypes as C
+
+    rng = np.random.default_rng(5)
+    n_msgs, first = 128, 126
+    bufs = [np.zeros(65535, np.uint8) for _ in range(n_msgs)]
+    for s in (126, 127):
+        bufs[s][: SEGS * MSG] = rng.integers(0, 256, SEGS * MSG, dtype=np.uint8)
+    ctl = np.frombuffer(_gro_cmsg(MSG), np.uint8).copy()
+    u8p = C.POINTER(C.c_uint8)
+    cb = (u8p * n_msgs)(*[C.cast(b.ctypes.data, u8p) for b in bufs])
+    oobs = (u8p * n_msgs)(*[C.cast(ctl.ctypes.data, u8p)] * n_msgs)
+    nns = (C.c_size_t * n_msgs)(*([0] * first + [len(ctl)] * 2))
+    ns = (C.c_int * n_msgs)()
+    src = (C.c_int * n_msgs)()
+    npk = C.c_int(0)
+
+    def reset():
+        for i in range(n_msgs):
+            ns[i] = SEGS * MSG if i >= first else 0
+
+    def timed(fn):
+        ts = []
+        for _ in range(reps):
+            reset()
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
+    gpu = timed(lambda: dev.lib.wgcs_split_messages(dev.h, cb, 65535, ns, oobs, nns, n_msgs, first, src,
+                                                    C.byref(npk)))
+    assert npk.value == 90
+    out = {"call": "wgcs_split_messages, one recvmmsg batch (2 x 45 x 1452 B -> 90 packets), host buffers",
+           "median_us": round(gpu * 1e6, 1)}
+    if with_cpu:
+        oracle = _oracle()
+        O = oracle._conn_lib()
+        arr = (oracle._OrMsg * n_msgs)()
+
+        def cpu():
+            for i in range(n_msgs):
+                arr[i] = oracle._OrMsg(bufs[i].ctypes.data, 65535, 65535, ns[i], ctl.ctypes.data, len(ctl), len(ctl),
+                                       nns[i], i)
+            O.or_split_messages(arr, n_msgs, first, C.byref(npk))
+
+        out["cpu_oracle_median_us"] = round(timed(cpu) * 1e6, 1)
+        out["cpu_oracle_note"] = "includes ~128 ctypes struct fills per call"
+    return out
+
+
+def split_cpu_baseline(srcs, seconds, B=16, n_msgs=128, first=126):
+    """The oracle (C restatement of splitMessages) on B batches of the same
+    shape, 1 thread, for `seconds`."""
+    import ctypes as C
+
+    oracle = _oracle()
+    L = oracle._conn_lib()
+    L.or_split_batch.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                 C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    L.or_split_batch.restype = None
+    ns_ = n_msgs - first
+    bufs = np.zeros((B * n_msgs, 65535), np.uint8)
+    ns0 = np.zeros(B * n_msgs, np.int32)
+    oobs = np.zeros((B * n_msgs, 24), np.uint8)
+    nns = np.zeros(B * n_msgs, np.int32)
+    for b in range(B):
+        for t in range(ns_):
+            q = b * n_msgs + first + t
+            bufs[q, : SEGS * MSG] = srcs[b * ns_ + t]
+            ns0[q] = SEGS * MSG
+            oobs[q] = np.frombuffer(_gro_cmsg(MSG), np.uint8)
+            nns[q] = 24
+    cnt = np.zeros(B, np.int32)
+    st = np.zeros(B, np.int32)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        ns = ns0.copy()
+        L.or_split_batch(bufs.ctypes.data, 65535, 65535, ns.ctypes.data, oobs.ctypes.data, 24, nns.ctypes.data,
+                         n_msgs, first, B, cnt.ctypes.data, st.ctypes.data)
+        reps += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    assert (cnt == ns_ * SEGS).all() and (st == 0).all()
+    bps = 2 * B * ns_ * SEGS * MSG
+    return {"value": round(bps * reps / dt / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} passes over {B} recvmmsg batches of the same shape, {dt:.1f} s, "
+                      "C restatement of splitMessages (bytes read + written)"}
+
+
+# ------------------------------------------------------------------ coalesce
+def run_coalesce(args, torch, dev, rank, world, barrier, B=1024, max_bufs=128):
+    import os
+
+    stride, cap = int(os.environ.get("WGCS_UDP_STRIDE", 65536)), 65535
+    rng = np.random.default_rng(synth.SEED + 88 + rank)
+    R = 2
+    pk = rng.integers(0, 256, (B * max_bufs, MSG), dtype=np.uint8)
+    stream = torch.cuda.Stream()
+    d_bufs = []
+    for _ in range(R):
+        t = torch.zeros((B * max_bufs, stride), dtype=torch.uint8, device="cuda")
+        t[:, :MSG].copy_(torch.from_numpy(pk))
+        d_bufs.append(t)
+    d_lens = torch.full((B * max_bufs,), MSG, dtype=torch.int32, device="cuda")
+    d_nb = torch.full((B,), max_bufs, dtype=torch.int32, device="cuda")
+    d_nm = torch.zeros(B, dtype=torch.int32, device="cuda")
+    d_first, d_len, d_gso = (torch.zeros(B * max_bufs, dtype=torch.int32, device="cuda") for _ in range(3))
+    L, h, s = dev.lib, dev.h, stream.cuda_stream
+
+    def step(k):
+        i = k % R
+        rc = L.wgcs_coalesce_messages_batch(h, d_bufs[i].data_ptr(), stride, cap, None, d_lens.data_ptr(),
+                                            d_nb.data_ptr(), max_bufs, B, 0, d_nm.data_ptr(), d_first.data_ptr(),
+                                            d_len.data_ptr(), d_gso.data_ptr(), s)
+        assert rc == 0
+
+    elapsed, kern_ms = _time_steps(torch, stream, step, args.steps, args.warmup, barrier)
+    nm = d_nm.cpu().numpy()
+    assert (nm == 3).all(), nm[:4]
+    runs = [SEGS, SEGS, max_bufs - 2 * SEGS]
+    ml = d_len.view(B, max_bufs)[:, :3].cpu().numpy()
+    assert (ml == np.array(runs) * MSG).all()
+    for b in (0, B // 2, B - 1):  # the first buffer of run r holds packets f..f+n-1 back to back
+        f = 0
+        for n in runs:
+            got = d_bufs[0][b * max_bufs + f, : n * MSG].cpu().numpy()
+            assert np.array_equal(got, pk[b * max_bufs + f: b * max_bufs + f + n].reshape(-1)), (b, f)
+            f += n
+    moved = B * (max_bufs - 3) * MSG
+    bps = 2 * moved
+    copy_ms = _copy_ms(torch, stream, d_bufs[1].view(-1), d_bufs[0].view(-1), moved, args.steps)
+    res = _result("device-resident UDP GSO coalesce GiB/s (bytes read + written), 1024 Send batches x 128 x 1452 B",
+                  args, f"{B} Send batches of {max_bufs} x {MSG}-B transport messages to an IPv4 peer -> "
+                  f"3 UDP_SEGMENT messages ({'/'.join(map(str, runs))} packets) each; coalesceMessages, "
+                  "conn/bind.go:599-662, in place (SURVEY.md §8f row 3)",
+                  {"batches": B, "packets_per_step": B * max_bufs, "moved_bytes": moved, "rotated_copies": R,
+                   "slot_stride": stride},
+                  "udp_coalesce_kernel<6>", kern_ms, bps, copy_ms, elapsed)
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        res["cpu_baseline"] = coalesce_cpu_baseline(pk, args.cpu_seconds)
+    return res
+
+
+def coalesce_cpu_baseline(pk, seconds, B=16, max_bufs=128):
+    import ctypes as C
+
+    oracle = _oracle()
+    L = oracle._conn_lib()
+    L.or_coalesce_batch.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                    C.c_int, C.c_void_p]
+    L.or_coalesce_batch.restype = None
+    bufs = np.zeros((B * max_bufs, 65536), np.uint8)
+    bufs[:, :MSG] = pk[: B * max_bufs]
+    lens = np.full(B * max_bufs, MSG, np.uint64)
+    caps = np.full(B * max_bufs, 65535, np.uint64)
+    nb = np.full(B, max_bufs, np.int32)
+    nm = np.zeros(B, np.int32)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        L.or_coalesce_batch(bufs.ctypes.data, 65536, lens.ctypes.data, caps.ctypes.data, nb.ctypes.data, max_bufs, B,
+                            0, nm.ctypes.data)
+        reps += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    assert (nm == 3).all()
+    bps = 2 * B * (max_bufs - 3) * MSG
+    return {"value": round(bps * reps / dt / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} passes over {B} Send batches of the same shape, {dt:.1f} s, "
+                      "C restatement of coalesceMessages (bytes read + written)"}
