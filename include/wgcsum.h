@@ -221,7 +221,8 @@ int wgcs_get_gso_size(const uint8_t *control, size_t len, int *gso_size);
 int wgcs_set_gso_size(uint8_t *control, size_t *len, size_t cap, uint16_t gso_size);
 
 /* splitMessages over n_batches recvmmsg batches of n_msgs messages each.
- * Message slot q = b*n_msgs + s.  Input: the recvmmsg landing buffers only --
+ * At most 128 source messages (n_msgs - first_msg_at <= 128; BatchSize is 128,
+ * conn/conn.go:14).  Message slot q = b*n_msgs + s.  Input: the recvmmsg landing buffers only --
  * msgs[s].Buffers[0] for s >= first_msg_at (buf_len bytes, len == cap) at
  * d_in + (b*(n_msgs - first_msg_at) + s - first_msg_at)*in_stride;
  * d_n_in[q] = msgs[s].N (all s), d_gso[q] = getGSOSize result (>= 0) or WGCS_ERR_CMSG.

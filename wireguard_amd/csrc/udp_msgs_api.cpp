@@ -92,8 +92,9 @@ int wgcs_split_messages_batch(wgcs_ctx* ctx, const uint8_t* d_in, uint64_t in_st
   if (n_batches == 0 || n_msgs == 0) return WGCS_OK;
   if (!d_in || !d_n_in || !d_gso || !d_out || !d_n_out || !d_src || !d_count || !d_status)
     return set_err(ctx, WGCS_ERR_INVALID_ARG, "NULL pointer");
-  if (first_msg_at > n_msgs || buf_len > 0x7FFFFFFFu || (out_stride & 15) || ((uintptr_t)d_out & 15))
-    return set_err(ctx, WGCS_ERR_INVALID_ARG, "first_msg_at / buf_len / 16-byte aligned output slots");
+  if (first_msg_at > n_msgs || n_msgs - first_msg_at > 128 || buf_len > 0x7FFFFFFFu || (out_stride & 15) ||
+      ((uintptr_t)d_out & 15))
+    return set_err(ctx, WGCS_ERR_INVALID_ARG, "first_msg_at (<= 128 sources) / buf_len / 16-byte aligned output slots");
   std::lock_guard<std::mutex> g(ctx->mu);
   hipSetDevice(ctx->device);
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
@@ -129,6 +130,7 @@ int wgcs_split_messages(wgcs_ctx* ctx, uint8_t* const* bufs, size_t buf_len, int
   if (!ctx || !n_packets) return WGCS_ERR_INVALID_ARG;
   *n_packets = 0;
   if (n_msgs <= 0 || !bufs || !ns || !addr_src || first_msg_at < 0 || first_msg_at > n_msgs ||
+      n_msgs - first_msg_at > 128 ||
       buf_len > 0x7FFFFFFFu || (!oobs && first_msg_at < n_msgs) || (!nns && first_msg_at < n_msgs))
     return set_err(ctx, WGCS_ERR_INVALID_ARG, "bufs/ns/oobs/first_msg_at");
   const int nsrc = n_msgs - first_msg_at;

@@ -55,6 +55,9 @@ __device__ __forceinline__ uint4 ld16_nt(const uint8_t* p) {
 // Full 16-byte chunks go out as one dwordx4 (non-temporal with
 // WGCS_UDP_NTS: the packets are not re-read by this kernel); partial chunks
 // through store_chunk's byte-exact pieces.
+#ifndef WGCS_UDP_COAL_ROWS
+#define WGCS_UDP_COAL_ROWS 16  // buffers (16-lane rows) per coalesce block (16: 85 us, 32: 93 us, 64: 102 us on the bench)
+#endif
 #ifndef WGCS_UDP_NTS
 #define WGCS_UDP_NTS 0
 #endif
@@ -194,15 +197,16 @@ __global__ __launch_bounds__(256) void udp_split_kernel(const uint8_t* __restric
 
 // ---------------------------------------------------------------------------
 // coalesceMessages (conn/bind.go:599-662) over n_batches sendmmsg batches, in
-// place.  Block = 1024 threads = 64 rows = 64 consecutive buffers of one
-// batch; grid = (batch, buffer group).  Every row first loads its buffer's
+// place.  Block = ROWS x 16 threads = ROWS consecutive buffers of one batch
+// (ROWS = 16 by default: more, smaller blocks per CU keep loads and stores of
+// different blocks overlapped); grid = (batch, buffer group).  Every row first loads its buffer's
 // first 16*U source chunks (aligned; they need only len(bufs[j])), while wave
 // 0 replays the coalescing loop over the batch's lengths and publishes each
 // of the block's buffers' destination offset through LDS.  After the barrier
 // a row whose buffer was appended shifts its chunks to the destination phase
 // (previous lane's chunk via DPP row_ror:1 + funnel) and stores them.
-template <int U>
-__global__ __launch_bounds__(1024) void udp_coalesce_kernel(uint8_t* __restrict__ bufs, uint64_t stride,
+template <int U, int ROWS>
+__global__ __launch_bounds__(ROWS * 16) void udp_coalesce_kernel(uint8_t* __restrict__ bufs, uint64_t stride,
                                                             uint32_t buf_cap, const int32_t* __restrict__ caps,
                                                             const int32_t* __restrict__ lens,
                                                             const int32_t* __restrict__ nbufs_arr, uint32_t max_bufs,
@@ -210,13 +214,13 @@ __global__ __launch_bounds__(1024) void udp_coalesce_kernel(uint8_t* __restrict_
                                                             int32_t* __restrict__ msg_first,
                                                             int32_t* __restrict__ msg_len,
                                                             int32_t* __restrict__ msg_gso) {
-  __shared__ int64_t s_dst[64];  // destination byte offset of the row's buffer, or -1 (not moved)
+  __shared__ int64_t s_dst[ROWS];  // destination byte offset of the row's buffer, or -1 (not moved)
   const int lane = threadIdx.x & 63, r = lane & 15;
   const int wv = threadIdx.x >> 6;
   const uint32_t b = blockIdx.x;
   const uint64_t slot0 = (uint64_t)b * max_bufs;
   const int nb = min(nbufs_arr[b], (int)max_bufs);
-  const int jb0 = (int)blockIdx.y * 64;
+  const int jb0 = (int)blockIdx.y * ROWS;
   const int row = wv * 4 + (lane >> 4);
   const int j = jb0 + row;  // this row's buffer
 
@@ -255,7 +259,7 @@ __global__ __launch_bounds__(1024) void udp_coalesce_kernel(uint8_t* __restrict_
       for (int t = 0; t < cend;) {
         const int jj = c0 + t;
         const int bl = rl(vl, t);
-        const bool mine = jj >= jb0 && jj < jb0 + 64;
+        const bool mine = jj >= jb0 && jj < jb0 + ROWS;
         if (jj > 0 && bl + mlen <= maxp && bl <= gso && bl <= mcap - mlen && npk < kMaxUdpSegments &&
             !end_batch) {  // :620-643 append
           int m = 1;
@@ -276,7 +280,7 @@ __global__ __launch_bounds__(1024) void udp_coalesce_kernel(uint8_t* __restrict_
           }
           const int64_t dbase = (int64_t)(slot0 + (uint64_t)first) * (int64_t)stride + mlen;
           const int jl = c0 + lane;
-          if (lane >= t && lane < t + m && jl >= jb0 && jl < jb0 + 64)
+          if (lane >= t && lane < t + m && jl >= jb0 && jl < jb0 + ROWS)
             s_dst[jl - jb0] = dbase + (int64_t)(lane - t) * bl;
           (void)mine;
           mlen += m * bl;
@@ -361,8 +365,9 @@ hipError_t launch_udp_coalesce(uint8_t* bufs, uint64_t stride, uint32_t buf_cap,
                                int dst_is_v6, int32_t* n_msgs, int32_t* msg_first, int32_t* msg_len,
                                int32_t* msg_gso, hipStream_t s) {
   if (n_batches == 0 || max_bufs == 0) return hipSuccess;
-  const dim3 grid(n_batches, (max_bufs + 63) / 64);
-  hipLaunchKernelGGL(udp_coalesce_kernel<6>, grid, dim3(1024), 0, s, bufs, stride, buf_cap, caps, lens, nbufs,
+  constexpr int kRows = WGCS_UDP_COAL_ROWS;
+  const dim3 grid(n_batches, (max_bufs + kRows - 1) / kRows);
+  hipLaunchKernelGGL((udp_coalesce_kernel<6, kRows>), grid, dim3(kRows * 16), 0, s, bufs, stride, buf_cap, caps, lens, nbufs,
                      max_bufs, dst_is_v6, n_msgs, msg_first, msg_len, msg_gso);
   return hipGetLastError();
 }

@@ -308,7 +308,7 @@ def run_coalesce(args, torch, dev, rank, world, barrier, B=1024, max_bufs=128):
                   "conn/bind.go:599-662, in place (SURVEY.md §8f row 3)",
                   {"batches": B, "packets_per_step": B * max_bufs, "moved_bytes": moved, "rotated_copies": R,
                    "slot_stride": stride},
-                  "udp_coalesce_kernel<6>", kern_ms, bps, copy_ms, elapsed)
+                  "udp_coalesce_kernel<6,16>", kern_ms, bps, copy_ms, elapsed)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         res["cpu_baseline"] = coalesce_cpu_baseline(pk, args.cpu_seconds)
     return res
