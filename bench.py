@@ -153,7 +153,7 @@ def main():
     if scaling == "strong":
         total_bytes = int(n_cfg) * flen * args.steps
     value = total_bytes / elapsed / 2**30
-    kname = "checksum_batch_kernel<VALIDATE,16,6,nt>" if mode == MODE_VALIDATE else "checksum_batch_kernel<L4_FILL,16,6,nt>"
+    kname = f"checksum_batch_kernel<{'VALIDATE' if mode == MODE_VALIDATE else 'L4_FILL'},{_tune_tag()},nt>"
     result = {
         "metric": "device-resident payload GiB/s, Internet checksum, 64k×1500B batch",
         "value": round(value, 2),
@@ -203,6 +203,21 @@ def main():
     dev.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _tune_tag():
+    """G,U of the launched checksum kernel: the library defaults (wgcs_kernels.h
+    LaunchTuning: 32 lanes per packet, 4 loads in flight per lane) or the
+    WGCS_LANES_PER_PKT / WGCS_UNROLL overrides api.cpp reads."""
+    g = int(os.environ.get("WGCS_LANES_PER_PKT", "32"))
+    u = int(os.environ.get("WGCS_UNROLL", "4"))
+    if g == 32:
+        u = 6 if u >= 6 else (4 if u >= 4 else 3)
+    elif g == 64:
+        u = 4 if u >= 4 else 2
+    else:
+        g, u = 16, (8 if u >= 8 else (6 if u >= 6 else 4))
+    return f"{g},{u}"
 
 
 def traffic_per_launch(kname, algo_bytes):

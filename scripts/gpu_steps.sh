@@ -28,7 +28,7 @@ for s in "$@"; do
     tests-conn) step tests_conn 400 python -u -m pytest tests/test_gpu_conn.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     bench-usplit) step bench_usplit 300 python bench.py --config udp_split --steps 100 --warmup 10 --cpu-seconds 5 ;;
     bench-ucoal) step bench_ucoal 300 python bench.py --config udp_coalesce --steps 100 --warmup 10 --cpu-seconds 5 ;;
-    prof-udp) (cd /tmp && step prof_usplit 300 rocprofv3 --kernel-trace --stats -d "$OUT/profusplit_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config udp_split --steps 50 --warmup 5 --cpu-seconds 0) && (cd /tmp && step prof_ucoal 300 rocprofv3 --kernel-trace --stats -d "$OUT/profucoal_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config udp_coalesce --steps 50 --warmup 5 --cpu-seconds 0) ;;
+    prof-udp) (cd /tmp && step prof_usplit 300 rocprofv3 --kernel-trace --stats -d "$OUT/profusplit_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config udp_split --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e) && (cd /tmp && step prof_ucoal 300 rocprofv3 --kernel-trace --stats -d "$OUT/profucoal_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config udp_coalesce --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e) ;;
     sweep) step sweep 400 python scripts/sweep_checksum.py ;;
     sweep-align) step sweep_align 400 python scripts/sweep_checksum.py --variants 16:6:8:1:16,16:6:8:1:64,16:6:8:1:128,16:8:8:1:16,16:8:8:1:64,16:8:8:1:128 ;;
     sweep-cfg3) step sweep_cfg3 400 python scripts/sweep_checksum.py --config cfg3 ;;
@@ -44,7 +44,7 @@ for s in "$@"; do
     prof) (cd /tmp && step prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e) ;;
     pmc) (cd /tmp && step pmc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e --no-event-timing) ;;
     pmc-w) (cd /tmp && step pmcw 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e --no-event-timing) ;;
-    prof-cfg4) (cd /tmp && step prof_cfg4 400 rocprofv3 --kernel-trace --stats -d "$OUT/profcfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 50 --warmup 5 --cpu-seconds 0) ;;
+    prof-cfg4) (cd /tmp && step prof_cfg4 400 rocprofv3 --kernel-trace --stats -d "$OUT/profcfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e) ;;
     pmc-sq-cfg4) (cd /tmp && step pmcsq_cfg4 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace -d "$OUT/pmcsqcfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 20 --warmup 2 --cpu-seconds 0) ;;
     pmc-sq2-cfg4) (cd /tmp && step pmcsq2_cfg4 400 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcsq2cfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 20 --warmup 2 --cpu-seconds 0) ;;
     pmc-sq) (cd /tmp && step pmcsq 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD --kernel-trace -d "$OUT/pmcsq_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --cpu-seconds 0) ;;

@@ -14,6 +14,7 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 
@@ -34,8 +35,9 @@ def main():
     fs, ws = counter(fdir, "FETCH_SIZE"), counter(wdir, "WRITE_SIZE")
     res = {}
     for k, v in fs.items():
-        mode = "VALIDATE" if "<2," in k else ("L4_FILL" if "<1," in k else k)
-        key = f"checksum_batch_kernel<{mode},16,6,nt>"
+        targs = re.search(r"checksum_batch_kernel<(\d+), (\d+), (\d+), (true|false)>", k)
+        mode = {"2": "VALIDATE", "1": "L4_FILL"}.get(targs.group(1), targs.group(1))
+        key = f"checksum_batch_kernel<{mode},{targs.group(2)},{targs.group(3)},{'nt' if targs.group(4) == 'true' else 'rt'}>"
         rd = statistics.median(v) * 1024 * 2
         wr = statistics.median(ws.get(k, [0.0])) * 1024
         res[key] = {"hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),

@@ -32,6 +32,7 @@ for v in a.variants.split(","):
     os.environ["WGCS_LANES_PER_PKT"], os.environ["WGCS_UNROLL"], os.environ["WGCS_BLOCKS_PER_CU"] = g, u, b
     os.environ["WGCS_NT"] = nt
     os.environ["WGCS_ALIGN"] = f[4] if len(f) > 4 else "16"
+    os.environ["WGCS_FLAT"] = f[5] if len(f) > 5 else "0"
     devs[v] = Device(0)
 res = {v: [] for v in devs}
 for r in range(a.rounds):
@@ -50,6 +51,6 @@ for r in range(a.rounds):
             assert bool(out[:n].all().item()), v
 for v, t in res.items():
     t = np.array(t)
-    print(json.dumps({"variant(G:U:BPC:NT[:ALIGN])": v, "config": a.config, "median_us": round(float(np.median(t)), 2),
+    print(json.dumps({"variant(G:U:BPC:NT[:ALIGN[:FLAT]])": v, "config": a.config, "median_us": round(float(np.median(t)), 2),
                       "min_us": round(float(t.min()), 2), "GBps": round(nbytes / np.median(t) / 1e3, 1),
                       "frac_8TBs": round(nbytes / np.median(t) / 1e3 / 8000, 3)}))

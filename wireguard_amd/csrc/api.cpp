@@ -100,9 +100,11 @@ int wgcs_init(int device, wgcs_ctx** out) {
   const char* unr = getenv("WGCS_UNROLL");
   if (unr && atoi(unr) > 0) ctx->tune.unroll = atoi(unr);
   const char* lpp = getenv("WGCS_LANES_PER_PKT");
-  if (lpp && atoi(lpp) == 64) ctx->tune.lanes_per_pkt = 64;
+  if (lpp && (atoi(lpp) == 64 || atoi(lpp) == 32)) ctx->tune.lanes_per_pkt = atoi(lpp);
   const char* nt = getenv("WGCS_NT");
   if (nt) ctx->tune.nt = atoi(nt) ? 1 : 0;
+  const char* fl = getenv("WGCS_FLAT");
+  if (fl) ctx->tune.flat = atoi(fl) ? 1 : 0;
   const char* al = getenv("WGCS_ALIGN");
   if (al && (atoi(al) == 16 || atoi(al) == 32 || atoi(al) == 64 || atoi(al) == 128)) ctx->tune.align = atoi(al);
   *out = ctx;

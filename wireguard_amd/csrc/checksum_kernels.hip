@@ -59,6 +59,161 @@ __device__ __forceinline__ uint4 ld_chunk(const uint4* p) {
   return *p;
 }
 
+// ---------------------------------------------------------------------------
+// Flat path (VALIDATE / L4_FILL, 16-lane rows): when the wave's 4 packets lie
+// back to back in the arena and each packet's summed bytes form ONE range --
+// the pseudo-header addresses directly followed by the L4 segment
+// ([12, len) for IPv4 with IHL 5, [8, len) for IPv6 without extension
+// headers; L4_FILL also skips the 2-byte checksum field) -- the wave streams
+// the 4 packets as one run: every load instruction reads 1 KiB of consecutive
+// bytes (the flat-stream access pattern) and each chunk is
+// attributed to its packet.  Chunks that straddle a range boundary or the
+// field ("dirty", at most 3 per packet) take a masked path; the dirty set is
+// a wave-uniform bitmask per load instruction built from the boundaries.
+// Any other group (gaps, IP options, short packets) uses the row path.
+struct FlatGroup {
+  int lo[4], hi[4], hole[4];  // positions relative to the aligned run base
+  int nch;
+  const uint4* src;
+};
+
+template <int MODE, int U, bool NT>
+__device__ __forceinline__ bool flat_group(uint8_t* __restrict__ arena, const wgcs_pkt& d, uint32_t base, uint32_t n,
+                                           void* __restrict__ out, int inplace, int lane) {
+  if (base + 4 > n) return false;
+  // the 4 descriptors (row q's lane 16q holds packet base + q) as scalars
+  uint64_t off[4];
+  int len[4], cs[4], co[4], fl[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t lo32 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)d.off, 16 * q);
+    const uint32_t hi32 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(d.off >> 32), 16 * q);
+    off[q] = ((uint64_t)hi32 << 32) | lo32;
+    len[q] = __builtin_amdgcn_readlane((int)d.len, 16 * q);
+    const uint32_t w = (uint32_t)d.csum_start | ((uint32_t)d.csum_offset << 16) | ((uint32_t)d.flags << 24);
+    const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane((int)w, 16 * q);
+    cs[q] = (int)(ws & 0xFFFFu);
+    co[q] = (int)((ws >> 16) & 0xFFu);
+    fl[q] = (int)(ws >> 24);
+  }
+  int alo[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const bool v6 = (fl[q] & WGCS_PKT_V6) != 0;
+    alo[q] = v6 ? 8 : 12;
+    if (cs[q] != (v6 ? 40 : 20) || len[q] < cs[q] + 8 || len[q] > 16384) return false;
+    if (MODE == WGCS_MODE_L4_FILL && cs[q] + co[q] + 2 > len[q]) return false;
+    if (q > 0 && off[q] != off[q - 1] + (uint64_t)len[q - 1]) return false;
+  }
+  // aligned run base: the first summed byte rounded down to 16
+  uint8_t* first = arena + off[0] + alo[0];
+  const int s0 = (int)((uintptr_t)first & 15u);
+  const uint4* src = reinterpret_cast<const uint4*>(first - s0);
+  int lo[4], hi[4], hole[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int rel = (int)(off[q] - off[0]) - alo[0] + s0;  // packet start relative to the run base
+    lo[q] = rel + alo[q];
+    hi[q] = rel + len[q];
+    hole[q] = MODE == WGCS_MODE_L4_FILL ? rel + cs[q] + co[q] : -64;
+  }
+  const int nch = (hi[3] + 15) >> 4;
+  uint32_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
+  for (int c0 = 0; c0 < nch; c0 += 64 * U) {  // wave-uniform
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + 64 * u + lane;
+      v[u] = c < nch ? ld_chunk<NT>(src + c) : make_uint4(0, 0, 0, 0);
+    }
+    // dirty-chunk masks of this window (wave-uniform, scalar)
+    uint64_t dm[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) dm[u] = 0;
+    auto mark = [&](int chunk) {
+      const int rc = chunk - c0;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (rc >= 64 * u && rc < 64 * u + 64) dm[u] |= 1ull << (rc - 64 * u);
+    };
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (lo[q] & 15) mark(lo[q] >> 4);
+      if (hi[q] & 15) mark(hi[q] >> 4);
+      if (MODE == WGCS_MODE_L4_FILL) {
+        mark(hole[q] >> 4);
+        mark((hole[q] + 1) >> 4);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + 64 * u + lane;
+      const int x = 16 * c;
+      const int f = (x >= hi[0]) + (x >= hi[1]) + (x >= hi[2]);
+      if (((dm[u] >> lane) & 1ull) == 0) {
+        if (c < nch && x >= lo[0]) {  // clean chunk: all 16 bytes summed into packet f
+          const uint32_t t = add_halves(add_halves(add_halves(add_halves(0u, v[u].x), v[u].y), v[u].z), v[u].w);
+          acc0 += f == 0 ? t : 0u;
+          acc1 += f == 1 ? t : 0u;
+          acc2 += f == 2 ? t : 0u;
+          acc3 += f == 3 ? t : 0u;
+        }
+      } else {
+        // dirty: masked shares of packets f and f + 1 (a 16-byte chunk meets at most two ranges)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int k = f + e;
+          if (k > 3) break;
+          const int klo = k == 0 ? lo[0] : (k == 1 ? lo[1] : (k == 2 ? lo[2] : lo[3]));
+          const int khi = k == 0 ? hi[0] : (k == 1 ? hi[1] : (k == 2 ? hi[2] : hi[3]));
+          const int kh = k == 0 ? hole[0] : (k == 1 ? hole[1] : (k == 2 ? hole[2] : hole[3]));
+          uint32_t m16 = byte_bits16(klo - x, khi - x);
+          if (MODE == WGCS_MODE_L4_FILL) m16 &= ~byte_bits16(kh - x, kh + 2 - x);
+          const uint32_t t = add_halves(add_halves(add_halves(add_halves(0u, v[u].x & expand_nibble(m16 & 0xFu)),
+                                                              v[u].y & expand_nibble((m16 >> 4) & 0xFu)),
+                                                   v[u].z & expand_nibble((m16 >> 8) & 0xFu)),
+                                        v[u].w & expand_nibble((m16 >> 12) & 0xFu));
+          acc0 += k == 0 ? t : 0u;
+          acc1 += k == 1 ? t : 0u;
+          acc2 += k == 2 ? t : 0u;
+          acc3 += k == 3 ? t : 0u;
+        }
+      }
+    }
+    acc0 = fold32_16(acc0);
+    acc1 = fold32_16(acc1);
+    acc2 = fold32_16(acc2);
+    acc3 = fold32_16(acc3);
+  }
+  // per packet: wave sum, parity (pairing from the packet's first summed byte), pseudo-header constant
+  uint32_t t4[4];
+  t4[0] = fold32_16(wave_sum_u32(acc0));
+  t4[1] = fold32_16(wave_sum_u32(acc1));
+  t4[2] = fold32_16(wave_sum_u32(acc2));
+  t4[3] = fold32_16(wave_sum_u32(acc3));
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t sq = t4[q];
+    if ((((uintptr_t)arena + off[q] + (uint64_t)alo[q]) & 1u) == 0) sq = bswap16(sq);
+    const uint32_t pre = ((fl[q] & WGCS_PKT_UDP) ? 17u : 6u) + ((uint32_t)(len[q] - cs[q]) & 0xFFFFu);
+    const uint32_t t = fold32_16(sq + pre);
+    if (lane == q) {
+      if (MODE == WGCS_MODE_VALIDATE) {
+        reinterpret_cast<uint8_t*>(out)[base + q] = (t == 0xFFFFu) ? 1 : 0;
+      } else {
+        const uint16_t cv = (uint16_t)~t;
+        reinterpret_cast<uint16_t*>(out)[base + q] = cv;
+        if (inplace) {
+          uint8_t* pkt = arena + off[q];
+          pkt[cs[q] + co[q]] = (uint8_t)(cv >> 8);
+          pkt[cs[q] + co[q] + 1] = (uint8_t)cv;
+        }
+      }
+    }
+  }
+  return true;
+}
+
 // One packet per group of G lanes (G = 16: 4 packets per wave in flight; G = 64:
 // one wavefront per packet).  The packet's 16-byte chunks are split into
 // "edge" chunks (the first ones, up to the end of the address range / gap /
@@ -66,13 +221,13 @@ __device__ __forceinline__ uint4 ld_chunk(const uint4* p) {
 // chunks that are summed unmasked: lanes stream interior chunk
 // c = c_lo + sub + G*(u + U*it), so one wave instruction reads 64/G
 // contiguous 16*G-byte runs, and each lane owns at most a few edge chunks.
-template <int MODE, int G, int U, bool NT>
+template <int MODE, int G, int U, bool NT, bool FLAT>
 __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict__ arena,
                                                              const wgcs_pkt* __restrict__ pkts,
                                                              const uint64_t* __restrict__ initial,
                                                              uint32_t n, void* __restrict__ out,
                                                              int inplace, uint32_t amask) {
-  static_assert(G == 16 || G == 64, "group = DPP row or wave");
+  static_assert(G == 16 || G == 32 || G == 64, "group = DPP row, half wave or wave");
   constexpr int PPW = 64 / G;  // packets per wave per step
   const int lane = threadIdx.x & 63;
   const int grp = lane / G;
@@ -90,6 +245,9 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
     const bool active = p < n;
     const wgcs_pkt d = dn;
     if (p + step < n) dn = pkts[p + step];  // prefetch the next descriptor
+    if constexpr (FLAT && G == 16 && (MODE == WGCS_MODE_VALIDATE || MODE == WGCS_MODE_L4_FILL)) {
+      if (flat_group<MODE, U, NT>(arena, d, base, n, out, inplace, lane)) continue;  // wave-uniform
+    }
     uint8_t* pkt = arena + d.off;
     const int len = active ? (int)d.len : 0;
     const int cs = d.csum_start;
@@ -172,7 +330,14 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
     }
     // all lanes converge here: per-lane fold, group sum, parity, pseudo/initial
     uint32_t s = fold32_16(acc);
-    s = (G == 16) ? row16_sum_u32(s) : wave_sum_u32(s);
+    if (G == 16) {
+      s = row16_sum_u32(s);
+    } else if (G == 32) {  // two DPP rows of the half wave: row sums, then the partner row's (lane ^ 16)
+      s = row16_sum_u32(s);
+      s += (uint32_t)__shfl_xor((int)s, 16);
+    } else {
+      s = wave_sum_u32(s);
+    }
     s = fold32_16(s);
     if (((pbase + (uintptr_t)r.main_lo) & 1u) == 0) s = bswap16(s);
     uint32_t t = fold32_16(s + pre + fold64_16(init));  // == the reference's checksum(...)
@@ -196,27 +361,35 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
 template <int MODE>
 static hipError_t launch_mode(uint8_t* arena, const wgcs_pkt* pkts, const uint64_t* init, uint32_t n, void* out,
                               int inplace, hipStream_t s, int num_cu, const LaunchTuning& t) {
-  const int ppb = (t.lanes_per_pkt == 64 ? 1 : 4) * 4;  // packets per block per step
+  const int ppb = (64 / t.lanes_per_pkt) * 4;  // packets per block per step
   long want = ((long)n + ppb - 1) / ppb;
   long cap = (long)num_cu * t.blocks_per_cu;
   const int grid = (int)(want < cap ? want : cap);
   const uint32_t amask = (uint32_t)(t.align >= 16 ? t.align : 16) - 1u;
-#define WGCS_LAUNCH(G, U)                                                                                        \
+#define WGCS_LAUNCH(G, U, FL)                                                                                      \
   do {                                                                                                            \
     if (t.nt)                                                                                                     \
-      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, true>), dim3(grid), dim3(256), 0, s, arena, pkts, init, \
-                         n, out, inplace, amask);                                                                 \
+      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, true, FL>), dim3(grid), dim3(256), 0, s, arena, pkts,  \
+                         init, n, out, inplace, amask);                                                           \
     else                                                                                                          \
-      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, false>), dim3(grid), dim3(256), 0, s, arena, pkts,    \
+      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, false, FL>), dim3(grid), dim3(256), 0, s, arena, pkts, \
                          init, n, out, inplace, amask);                                                           \
   } while (0)
   if (t.lanes_per_pkt == 64) {
-    if (t.unroll >= 4) WGCS_LAUNCH(64, 4);
-    else WGCS_LAUNCH(64, 2);
+    if (t.unroll >= 4) WGCS_LAUNCH(64, 4, false);
+    else WGCS_LAUNCH(64, 2, false);
+  } else if (t.lanes_per_pkt == 32) {
+    if (t.unroll >= 6) WGCS_LAUNCH(32, 6, false);
+    else if (t.unroll >= 4) WGCS_LAUNCH(32, 4, false);
+    else WGCS_LAUNCH(32, 3, false);
+  } else if (t.flat && (MODE == WGCS_MODE_VALIDATE || MODE == WGCS_MODE_L4_FILL)) {
+    if (t.unroll >= 8) WGCS_LAUNCH(16, 8, true);
+    else if (t.unroll >= 6) WGCS_LAUNCH(16, 6, true);
+    else WGCS_LAUNCH(16, 4, true);
   } else {
-    if (t.unroll >= 8) WGCS_LAUNCH(16, 8);
-    else if (t.unroll >= 6) WGCS_LAUNCH(16, 6);
-    else WGCS_LAUNCH(16, 4);
+    if (t.unroll >= 8) WGCS_LAUNCH(16, 8, false);
+    else if (t.unroll >= 6) WGCS_LAUNCH(16, 6, false);
+    else WGCS_LAUNCH(16, 4, false);
   }
 #undef WGCS_LAUNCH
   return hipGetLastError();

@@ -8,16 +8,18 @@
 // Mapping (gso_rows_kernel): one 16-lane DPP row per OUTPUT segment (slot =
 // job * max_segs + i), 64 segments per 1024-thread block, grid = (job,
 // segment group).  Every row first issues its payload loads (dword-aligned
-// 16-byte windows, U per lane in flight), which need only gsoSize; wave 0
-// meanwhile decodes the job (validation, geometry and the job-constant header
-// sums) and broadcasts it through LDS; then every row
-//   1. issues its header-chunk loads (L2-resident, shared by the job);
-//   2. shifts each window to the destination's byte phase (alignbyte with the
+// 16-byte windows, U per lane in flight, which need only gsoSize) and its
+// header-chunk loads (L2-resident, shared by the job); the decoder wave
+// meanwhile validates the job and publishes its geometry through LDS
+// (barrier 1), then computes the job-constant header sums (barrier 2) while
+// every row
+//   1. shifts each window to the destination's byte phase (alignbyte with the
 //      next lane's first dword via DPP row_ror), sums the L4 bytes from the
 //      same registers (v_dot2) and stores full global_store_dwordx4 chunks;
-//   3. computes the IPv4 and L4 checksums from the row sum plus the job
-//      constants and the rewritten field values, rewrites the header chunk
-//      and stores it last -- every output byte is written exactly once.
+//   2. after barrier 2, computes the IPv4 and L4 checksums from the row sum
+//      plus the job constants and the rewritten field values, rewrites the
+//      header chunk and stores it last -- every output byte is written once.
+// The barriers order LDS only (lds_barrier): loads stay in flight across them.
 // Reference quirks reproduced bit-for-bit: IPv4 ID is
 // id0 + 1 for every segment i >= 1; TCP seq uses a uint16 product
 // gsoSize * uint16(i); FIN/PSH cleared on all but the last segment; no UDP
@@ -375,9 +377,9 @@ __device__ __forceinline__ int ufl(int x) { return __builtin_amdgcn_readfirstlan
 
 // Row-per-segment split.  Block = 1024 threads = 64 rows of 16 lanes = 64
 // consecutive output segments of one job; grid = (job, segment group).
-// Wave 0 decodes the job (validation, geometry, job-constant header sums)
-// once and broadcasts it through LDS -- per-wave decoding made the CU's
-// shared scalar unit the bottleneck (16 decodes per CU).
+// One decoder wave decodes the job once and broadcasts it through LDS in two
+// steps (geometry, then the job-constant header sums) -- per-wave decoding
+// made the CU's shared scalar unit the bottleneck (16 decodes per CU).
 template <int U, bool NT>
 __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restrict__ arena,
                                                         const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
@@ -409,46 +411,44 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   const int dalign = (int)((uintptr_t)dst & 15u);
   uint8_t* dbase = dst - dalign;
 
-  // ---- wave 0: decode the job (validation, geometry, job-constant header
-  // sums) and publish it through LDS.  It runs before wave 0's own
-  // speculative loads: a decode step that waited on a global load would
-  // otherwise wait (vmcnt retires in order) for that whole payload batch.
+  // ---- decoder wave (the block's last: its rows are the least likely to
+  // exist, 45 segments per job at cfg4): validation and geometry, published
+  // through LDS at barrier 1; the job-constant header sums follow at barrier
+  // 2, computed while the other waves stream their payload.  It decodes
+  // before issuing its own speculative loads: a decode step that waited on a
+  // global load would otherwise wait (vmcnt retires in order) for that batch.
+  constexpr int kDec = 15;
   HdrBytes hb;
-  if (wv == 0) {
+  Job jd = {};
+  bool jd_ok = false;
+  if (wv == kDec) {
     hb.load(vb, (int)min(jlen, 256u), lane);
-    const Job j = decode_job(hb, jlen, jobs[jb].flags, room, max_segs);
-    const bool ok = j.status == 0 || j.status == WGCS_ERR_TOO_MANY_SEGMENTS;
-    HdrFast hf = {};
-    uint32_t id0 = 0, seq0 = 0;
-    if (ok && j.type != GSO_NONE) {  // wave-uniform: all lanes live
-      hf = header_fast(hb, j, lane);
-      id0 = j.ipv == 4 ? hb.be16(10 + 4) : 0u;
-      seq0 = j.type != GSO_UDP_L4 ? hb.be32(10 + j.cs + 4) : 0u;
-    }
+#if WGCS_GSO_EXP & 64
+    if (__builtin_amdgcn_readfirstlane((int)(hb.r0 + hb.r3)) == -1) hb.r1 = 0;  // stamp 5: header bytes arrived
+    GSO_STAMP(5);
+#endif
+    jd = decode_job(hb, jlen, jobs[jb].flags, room, max_segs);
+    jd_ok = jd.status == 0 || jd.status == WGCS_ERR_TOO_MANY_SEGMENTS;
     if (lane == 0) {
-      ji.status = j.status;
-      ji.count = ok ? j.count : 0;
-      ji.nseg = ok ? j.nseg : 0;
-      ji.type = j.type;
-      ji.ipv = j.ipv;
-      ji.hdr_len = j.hdr_len;
-      ji.gso = j.gso;
-      ji.cs = j.cs;
-      ji.co = j.co;
-      ji.plen = j.plen;
-      ji.flags = j.flags;
-      ji.fast = hf.fast ? 1 : 0;
-      ji.id0 = id0;
-      ji.seq0 = seq0;
-      ji.ip_base = hf.ip_base;
-      ji.l4_base = hf.l4_base;
-      ji.addr = hf.addr;
-      ji.tflags = hf.flags;
+      ji.status = jd.status;
+      ji.count = jd_ok ? jd.count : 0;
+      ji.nseg = jd_ok ? jd.nseg : 0;
+      ji.type = jd.type;
+      ji.ipv = jd.ipv;
+      ji.hdr_len = jd.hdr_len;
+      ji.gso = jd.gso;
+      ji.cs = jd.cs;
+      ji.co = jd.co;
+      ji.plen = jd.plen;
+      ji.flags = jd.flags;
       if (blockIdx.y == 0) {
         count[jb] = ji.count;
-        status[jb] = j.status;
+        status[jb] = jd.status;
       }
     }
+#if WGCS_GSO_EXP & 64
+    GSO_STAMP(6);
+#endif
   }
 
   // ---- speculative first payload batch.  The source window of segment i
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   // window picks up outside the segment are masked exactly as on the decoded
   // path (header positions, past pktLen).  GSO_NONE jobs skip it.
   int gso_s = 0, type_s = GSO_NONE;
-  if (wv == 0) {
+  if (wv == kDec) {
     if (jlen >= 10) {
       type_s = (int)hb(1);
       gso_s = (int)hb.le16(4);
@@ -487,8 +487,43 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
     if (ce >= vb && ce < jend) E = *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(ce, 4));
   }
 
-  __syncthreads();
+  // ---- speculative header chunks in packet coordinates (the fast path's;
+  // bytes past hdrLen are replaced by payload bytes later): L2 hits shared by
+  // the job's segments, issued after the payload batch so waiting for the
+  // payload does not wait for them.
+  const int hph_s = (int)((uintptr_t)rb & 15u);
+  const uint8_t* hab_s = rb - hph_s + 16 * r;
+  const uint8_t* hend_s = rb + min(plen_s, kMaxHdrLen + 16);
+  uint4 H0 = z, H1 = z;
+  if (spec) {
+    if (hab_s < hend_s) H0 = ld16(hab_s);
+    if (hab_s + 16 < hend_s) H1 = ld16(hab_s + 16);
+  }
+
+  lds_barrier();  // barrier 1: geometry; the speculative loads stay in flight
   GSO_STAMP(1);
+  // block-uniform: whether the header phase (and so barrier 2) happens at all
+  const bool hdr_phase = ufl(ji.nseg) > 0 && ufl(ji.type) != GSO_NONE;
+  if (wv == kDec && hdr_phase) {
+    const HdrFast hf = header_fast(hb, jd, lane);
+    const uint32_t id0 = jd.ipv == 4 ? hb.be16(10 + 4) : 0u;
+    const uint32_t seq0 = jd.type != GSO_UDP_L4 ? hb.be32(10 + jd.cs + 4) : 0u;
+    if (lane == 0) {
+      ji.fast = hf.fast ? 1 : 0;
+      ji.id0 = id0;
+      ji.seq0 = seq0;
+      ji.ip_base = hf.ip_base;
+      ji.l4_base = hf.l4_base;
+      ji.addr = hf.addr;
+      ji.tflags = hf.flags;
+    }
+#if WGCS_GSO_EXP & 64
+    GSO_STAMP(7);
+#endif
+    // barrier 2 (header constants).  Waves that retire early are not waited
+    // for: s_barrier only counts the workgroup's surviving waves.
+    lds_barrier();
+  }
   Job j = {};
   j.status = ufl(ji.status);
   j.nseg = ufl(ji.nseg);
@@ -509,10 +544,6 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   j.ipv = ufl(ji.ipv);
   j.hdr_len = ufl(ji.hdr_len);
   j.gso = ufl(ji.gso);
-  const bool fast = ufl(ji.fast) != 0;
-  const uint32_t id0 = (uint32_t)ufl((int)ji.id0), seq0 = (uint32_t)ufl((int)ji.seq0);
-  const uint32_t ip_base = (uint32_t)ufl((int)ji.ip_base), l4_base = (uint32_t)ufl((int)ji.l4_base);
-  const uint32_t addr_sum = (uint32_t)ufl((int)ji.addr), tflags = (uint32_t)ufl((int)ji.tflags);
   const bool v4 = j.ipv == 4, tcp = j.type != GSO_UDP_L4;
   if (i >= j.nseg) return;  // whole rows retire; DPP below stays inside live rows
   const bool spec_ok = spec && j.gso == gso_s;  // always true: both read virtio bytes 4-5
@@ -531,17 +562,6 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   const uint8_t* src_lo = rb + seg_start;
   const uint8_t* src_hi = rb + seg_end;
 
-  // ---- header source loads first (shared by the job's segments: L2 hits).
-  // fast: packet coordinates (lane r = readBuf[16r, 16r + 16), wave-uniform
-  // phase); general: destination coordinates (per-row phase).
-  const uint8_t* hend = rb + hdr_len;
-  const int hph = fast ? (int)((uintptr_t)rb & 15u) : (int)((uintptr_t)(rb - dalign) & 15u);
-  const uint8_t* hab = (fast ? rb : rb - dalign) - hph + 16 * r;
-  uint4 H0 = z, H1 = z;
-  if (r < hk) {
-    if (hab < hend && hab + 16 > rb) H0 = ld16(hab);
-    if (hab + 16 < hend && hab + 32 > rb) H1 = ld16(hab + 16);
-  }
 
   // ---- payload stream: destination chunk k = bytes [sb, sb + 16) of the
   // dword-aligned window k and the first dword of window k + 1 (next lane, DPP)
@@ -581,6 +601,29 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
     }
   }
   GSO_STAMP(3);
+
+  // ---- job-constant header sums (barrier 2; the decoder wave passed it already)
+  if (wv != kDec) lds_barrier();
+  const bool fast = ufl(ji.fast) != 0;
+  const uint32_t id0 = (uint32_t)ufl((int)ji.id0), seq0 = (uint32_t)ufl((int)ji.seq0);
+  const uint32_t ip_base = (uint32_t)ufl((int)ji.ip_base), l4_base = (uint32_t)ufl((int)ji.l4_base);
+  const uint32_t addr_sum = (uint32_t)ufl((int)ji.addr), tflags = (uint32_t)ufl((int)ji.tflags);
+
+  // ---- header source chunks (shared by the job's segments: L2 hits).
+  // fast: packet coordinates (lane r = readBuf[16r, 16r + 16), wave-uniform
+  // phase), normally the speculative H0/H1; general: destination coordinates
+  // (per-row phase).
+  const uint8_t* hend = rb + hdr_len;
+  const int hph = fast ? (int)((uintptr_t)rb & 15u) : (int)((uintptr_t)(rb - dalign) & 15u);
+  const uint8_t* hab = (fast ? rb : rb - dalign) - hph + 16 * r;
+  if (!fast || !spec_ok) {  // row-uniform
+    H0 = z;
+    H1 = z;
+    if (r < hk) {
+      if (hab < hend && hab + 16 > rb) H0 = ld16(hab);
+      if (hab + 16 < hend && hab + 32 > rb) H1 = ld16(hab + 16);
+    }
+  }
 
   const uint32_t id = i > 0 ? ((id0 + 1) & 0xFFFFu) : id0;  // quirk: id0 + 1 for every i >= 1 (:1426-1431)
   const uint32_t seq = seq0 + (uint32_t)(uint16_t)((uint16_t)j.gso * (uint16_t)i);  // uint16 product (:1445)

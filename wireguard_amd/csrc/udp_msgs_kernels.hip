@@ -314,7 +314,7 @@ __global__ __launch_bounds__(ROWS * 16) void udp_coalesce_kernel(uint8_t* __rest
       n_msgs_out[b] = i + 1;
     }
   }
-  __syncthreads();
+  lds_barrier();  // publishes s_dst; the speculative source loads stay in flight
   if (j >= nb || L == 0) return;
   const int64_t doff = s_dst[row];
   if (doff < 0) return;  // first buffer of a message: stays where it is

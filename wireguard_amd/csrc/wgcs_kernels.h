@@ -9,11 +9,12 @@
 namespace wgcs {
 
 struct LaunchTuning {
-  int blocks_per_cu = 8;   // 256-thread blocks per CU for the persistent grid
-  int lanes_per_pkt = 16;  // 16: one DPP row per packet (4 per wave); 64: one wave per packet
-  int unroll = 6;          // 16-byte loads in flight per lane per iteration
+  int blocks_per_cu = 16;  // 256-thread blocks per CU for the grid-stride grid
+  int lanes_per_pkt = 32;  // 16: one DPP row per packet (4 per wave); 32: half wave (2 per wave); 64: one wave
+  int unroll = 4;          // 16-byte loads in flight per lane per iteration
   int nt = 1;              // non-temporal (streaming) loads: each byte is read once
   int align = 16;          // chunk grid origin: packet start rounded down to this many bytes
+  int flat = 0;            // 16-lane rows only: stream back-to-back packet groups as one run (flat_group)
 };
 
 hipError_t launch_checksum_batch(int mode, unsigned flags, uint8_t* arena, const wgcs_pkt* pkts,

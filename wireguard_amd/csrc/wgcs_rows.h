@@ -65,4 +65,11 @@ __device__ __forceinline__ uint4 ld_window(const uint8_t* p, const uint8_t* hi) 
   return v;
 }
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS (and
+// scalar) operations, not for its outstanding global loads.  __syncthreads()'s
+// workgroup fence also drains vmcnt, which would expose the latency of loads
+// issued speculatively before the barrier.  The "memory" clobber keeps the
+// compiler from moving memory accesses across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 }  // namespace wgcs

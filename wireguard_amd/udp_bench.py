@@ -160,7 +160,7 @@ def run_split(args, torch, dev, rank, world, barrier, B=1024, n_msgs=128, first=
                   "conn/bind.go:542-597 (SURVEY.md §8f row 3)",
                   {"batches": B, "packets_per_step": B * ns * SEGS, "payload_bytes": payload, "rotated_copies": R},
                   "udp_split_kernel<6>", kern_ms, bps, copy_ms, elapsed)
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not getattr(args, "no_e2e", False):
         res["host_call"] = split_host_call(dev, with_cpu=args.cpu_seconds > 0)
         if args.cpu_seconds > 0:
             res["cpu_baseline"] = split_cpu_baseline(srcs, args.cpu_seconds)
