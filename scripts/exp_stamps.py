@@ -40,7 +40,7 @@ for k in range(8):
     v = S[:, k]
     m = v > 0
     out[f"t{k}_from_start"] = {q: int(np.percentile(v[m] - t0, q)) for q in (0, 10, 50, 90, 100)} if m.any() else None
-for a, b in ((0, 1), (1, 3), (3, 4), (0, 4), (0, 3), (0, 5), (5, 6), (6, 7), (7, 1)):
+for a, b in ((0, 1), (1, 3), (3, 4), (0, 4), (0, 3), (0, 5), (5, 2), (2, 6), (5, 6), (6, 7), (7, 1)):
     m = (S[:, a] > 0) & (S[:, b] > 0)
     d = S[m, b] - S[m, a]
     out[f"d{a}{b}"] = {q: int(np.percentile(d, q)) for q in (10, 50, 90)} if m.any() else None

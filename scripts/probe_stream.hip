@@ -121,3 +121,66 @@ extern "C" int probe_wavef_launch(const void* src, uint32_t npk, uint32_t stride
   else hipLaunchKernelGGL((probe_wavef<4>), dim3(grid), dim3(256), 0, s, (const uint8_t*)src, npk, stride, (uint32_t*)out);
   return (int)hipGetLastError();
 }
+
+// LDS-DMA stream (global_load_lds_dwordx4, 1 KiB per wave-instruction into a
+// wave-private 2-stage LDS ring), then ds_read_b128 of the lane's own slot:
+// does the DMA path read HBM faster than register loads (the guide's
+// ldsdma-fill row quotes 6.5-6.8 TB/s chip-wide with nt)?  Data is
+// wave-private, so one counted vmcnt + s_barrier orders it (4 waves per block
+// all run the same trip count: grid-stride by block).
+template <int U, int AUX>
+__global__ __launch_bounds__(256) void probe_glds(const uint4* __restrict__ src, size_t n16, uint32_t* __restrict__ out) {
+  __shared__ uint4 ring[4][2][U][64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t per_blk = (size_t)4 * U * 64;
+  const size_t nblk_items = (n16 + per_blk - 1) / per_blk;
+  uint32_t acc = 0;
+  size_t it = blockIdx.x;
+  auto issue = [&](size_t item, int stage) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      size_t c = item * per_blk + ((size_t)wv * U + u) * 64 + lane;
+      if (c >= n16) c = n16 - 1;
+      // asm, so hipcc does not count it and drain it with vmcnt(0) before the ds_read
+      const uint32_t lds_dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&ring[wv][stage][u][0];
+      const uint4* g = src + c;
+      uint32_t keep;
+      if (AUX == 2)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+      else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+    }
+  };
+  int stage = 0;
+  if (it < nblk_items) issue(it, 0);
+  for (; it < nblk_items; it += gridDim.x) {
+    const size_t nx = it + gridDim.x;
+    if (nx < nblk_items) {
+      issue(nx, stage ^ 1);
+      if (U == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if (U == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint4 v = ring[wv][stage][u][lane];
+      acc += v.x + v.y + v.z + v.w;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stage ^= 1;
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+extern "C" int probe_glds_launch(const void* src, size_t bytes, void* out, int grid, int u, int nt, void* stream) {
+  size_t n16 = bytes / 16;
+  hipStream_t s = (hipStream_t)stream;
+#define G(U, A) hipLaunchKernelGGL((probe_glds<U, A>), dim3(grid), dim3(256), 0, s, (const uint4*)src, n16, (uint32_t*)out)
+  if (nt) { if (u == 2) G(2, 2); else if (u == 4) G(4, 2); else G(8, 2); }
+  else { if (u == 2) G(2, 0); else if (u == 4) G(4, 0); else G(8, 0); }
+  return (int)hipGetLastError();
+}

@@ -161,6 +161,9 @@ __device__ Job decode_job(const HdrBytes& hb, uint32_t len, uint32_t jflags, uin
     count_segments(j, out_room, max_segs);
     return j;
   }
+#if WGCS_GSO_EXP & 64
+  GSO_STAMP(2);  // virtio fields and the job flags read
+#endif
   if (j.type == GSO_NONE) {  // tun/tun.go:532-556
     if (j.flags & 1) {
       const int at = (j.cs + j.co) & 0xFFFF;
@@ -393,8 +396,9 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   const int wv = threadIdx.x >> 6;
   const uint32_t jb = blockIdx.x;
   GSO_STAMP(0);
-  const uint8_t* vb = arena + jobs[jb].off;
-  const uint32_t jlen = jobs[jb].len;
+  const wgcs_gso_job job = jobs[jb];  // one scalar load of the whole descriptor, flags included
+  const uint8_t* vb = arena + job.off;
+  const uint32_t jlen = job.len;
   const uint8_t* rb = vb + 10;
   const uint64_t slot0 = (uint64_t)jb * max_segs;  // sizes[] index of segment 0
   // segment i of this job at out + obase + i * opitch (+ offset): fixed slots,
@@ -427,7 +431,7 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
     if (__builtin_amdgcn_readfirstlane((int)(hb.r0 + hb.r3)) == -1) hb.r1 = 0;  // stamp 5: header bytes arrived
     GSO_STAMP(5);
 #endif
-    jd = decode_job(hb, jlen, jobs[jb].flags, room, max_segs);
+    jd = decode_job(hb, jlen, job.flags, room, max_segs);
     jd_ok = jd.status == 0 || jd.status == WGCS_ERR_TOO_MANY_SEGMENTS;
     if (lane == 0) {
       ji.status = jd.status;
