@@ -58,16 +58,19 @@ def _time_steps(torch, stream, step, steps, warmup, barrier):
     return time.perf_counter() - t0, e0.elapsed_time(e1) / steps
 
 
-def _copy_ms(torch, stream, dst, src, nbytes, steps):
-    """Calibration: the runtime's device copy kernel moving the same bytes."""
+def _copy_ms(torch, stream, dsts, srcs, nbytes, steps):
+    """Calibration: the runtime's device copy kernel moving the same bytes,
+    rotated over the bench's buffer copies like the kernel's steps (one fixed
+    pair of ~134 MB buffers would be partly served by the 256 MB MALL)."""
+    R = len(dsts)
     with torch.cuda.stream(stream):
-        for _ in range(3):
-            dst[:nbytes].copy_(src[:nbytes])
+        for k in range(3):
+            dsts[k % R][:nbytes].copy_(srcs[k % R][:nbytes])
         c0 = torch.cuda.Event(enable_timing=True)
         c1 = torch.cuda.Event(enable_timing=True)
         c0.record(stream)
-        for _ in range(steps):
-            dst[:nbytes].copy_(src[:nbytes])
+        for k in range(steps):
+            dsts[k % R][:nbytes].copy_(srcs[k % R][:nbytes])
         c1.record(stream)
     torch.cuda.synchronize()
     return c0.elapsed_time(c1) / steps
@@ -153,7 +156,7 @@ def run_split(args, torch, dev, rank, world, barrier, B=1024, n_msgs=128, first=
         assert np.array_equal(got, srcs[b * ns:(b + 1) * ns].reshape(-1)), b
     payload = B * ns * SEGS * MSG
     bps = 2 * payload
-    copy_ms = _copy_ms(torch, stream, d_out[0].view(-1), d_in[0].view(-1), payload, args.steps)
+    copy_ms = _copy_ms(torch, stream, [o.view(-1) for o in d_out], [t.view(-1) for t in d_in], payload, args.steps)
     res = _result("device-resident UDP GRO split GiB/s (bytes read + written), 1024 recvmmsg batches x 2 x 45 x 1452 B",
                   args, f"{B} recvmmsg batches (BatchSize {n_msgs}, readAt {first}): {ns} UDP_GRO datagrams of "
                   f"{SEGS} x {MSG}-B transport messages each -> {ns * SEGS} packets per batch; splitMessages, "
@@ -301,7 +304,8 @@ def run_coalesce(args, torch, dev, rank, world, barrier, B=1024, max_bufs=128):
             f += n
     moved = B * (max_bufs - 3) * MSG
     bps = 2 * moved
-    copy_ms = _copy_ms(torch, stream, d_bufs[1].view(-1), d_bufs[0].view(-1), moved, args.steps)
+    flat = d_bufs[1].view(-1)  # disjoint regions of the (multi-GB) buffer: 4 x moved bytes, beyond the MALL
+    copy_ms = _copy_ms(torch, stream, [flat[moved:], flat[3 * moved:]], [flat, flat[2 * moved:]], moved, args.steps)
     res = _result("device-resident UDP GSO coalesce GiB/s (bytes read + written), 1024 Send batches x 128 x 1452 B",
                   args, f"{B} Send batches of {max_bufs} x {MSG}-B transport messages to an IPv4 peer -> "
                   f"3 UDP_SEGMENT messages ({'/'.join(map(str, runs))} packets) each; coalesceMessages, "
