@@ -31,6 +31,7 @@ for s in "$@"; do
     prof-udp) (cd /tmp && step prof_usplit 300 rocprofv3 --kernel-trace --stats -d "$OUT/profusplit_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config udp_split --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e) && (cd /tmp && step prof_ucoal 300 rocprofv3 --kernel-trace --stats -d "$OUT/profucoal_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config udp_coalesce --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e) ;;
     sweep) step sweep 400 python scripts/sweep_checksum.py ;;
     probe-glds) step probe_glds 300 python scripts/probe_glds.py ;;
+    probe-rows) step probe_rows 300 python scripts/probe_rows.py ;;
     sweep-align) step sweep_align 400 python scripts/sweep_checksum.py --variants 16:6:8:1:16,16:6:8:1:64,16:6:8:1:128,16:8:8:1:16,16:8:8:1:64,16:8:8:1:128 ;;
     sweep-cfg3) step sweep_cfg3 400 python scripts/sweep_checksum.py --config cfg3 ;;
     probe) step probe 400 python scripts/probe_stream.py ;;

@@ -184,3 +184,55 @@ extern "C" int probe_glds_launch(const void* src, size_t bytes, void* out, int g
   else { if (u == 2) G(2, 0); else if (u == 4) G(4, 0); else G(8, 0); }
   return (int)hipGetLastError();
 }
+
+// G-lane rows (G = 32: two packets per wave), U loads in flight per lane, grid-
+// stride over packets like checksum_batch_kernel<.., G, U, ..>, minus all
+// per-packet arithmetic.  DESC: the packet's offset and length come from a
+// 16-byte descriptor array (a dependent load before the data loads), as in
+// the kernel; otherwise they are computed from the index.
+template <int G, int U, bool DESC>
+__global__ __launch_bounds__(256) void probe_rowsg(const uint8_t* __restrict__ arena, const uint4* __restrict__ desc,
+                                                   uint32_t npk, uint32_t stride, uint32_t* __restrict__ out) {
+  constexpr int PPW = 64 / G;
+  const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t nw = gridDim.x * 4;
+  const int lane = threadIdx.x & 63, grp = lane / G, sub = lane % G;
+  uint32_t acc = 0;
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  for (uint32_t base = wave * PPW; base < npk; base += nw * PPW) {
+    const uint32_t p = base + grp;
+    uint64_t off = (uint64_t)p * stride;
+    uint32_t len = stride;
+    if (DESC) {
+      const uint4 d = p < npk ? desc[p] : make_uint4(0, 0, 0, 0);
+      off = ((uint64_t)d.y << 32) | d.x;
+      len = d.z;
+    }
+    const uint8_t* pkt = arena + off;
+    const int rel0 = 12 - (int)(((uintptr_t)pkt + 12) & 15);
+    const int nch = p < npk ? ((int)len - rel0 + 15) >> 4 : 0;
+    const u4* src = (const u4*)(pkt + rel0);
+    for (int c0 = sub; c0 < nch; c0 += G * U) {
+      u4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int c = c0 + G * u;
+        v[u] = c < nch ? __builtin_nontemporal_load(src + c) : u4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+extern "C" int probe_rowsg_launch(const void* src, const void* desc, uint32_t npk, uint32_t stride, void* out,
+                                  int grid, int g, int u, int use_desc, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define RG(G_, U_, D_) hipLaunchKernelGGL((probe_rowsg<G_, U_, D_>), dim3(grid), dim3(256), 0, s, (const uint8_t*)src, (const uint4*)desc, npk, stride, (uint32_t*)out)
+  if (g == 16) { if (use_desc) RG(16, 6, true); else RG(16, 6, false); }
+  else if (g == 32) {
+    if (u == 3) { if (use_desc) RG(32, 3, true); else RG(32, 3, false); }
+    else { if (use_desc) RG(32, 4, true); else RG(32, 4, false); }
+  } else { if (use_desc) RG(64, 2, true); else RG(64, 2, false); }
+  return (int)hipGetLastError();
+}
