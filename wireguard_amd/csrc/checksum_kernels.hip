@@ -67,9 +67,9 @@ __device__ __forceinline__ uint4 ld_chunk(const uint4* p) {
 // headers; L4_FILL also skips the 2-byte checksum field) -- the wave streams
 // the 4 packets as one run: every load instruction reads 1 KiB of consecutive
 // bytes (the flat-stream access pattern) and each chunk is
-// attributed to its packet.  Chunks that straddle a range boundary or the
-// field ("dirty", at most 3 per packet) take a masked path; the dirty set is
-// a wave-uniform bitmask per load instruction built from the boundaries.
+// attributed to its packet with a branch-free test.  Chunks that straddle a
+// range boundary or the field ("dirty", at most 4 per packet) contribute 0 in
+// the stream and are settled once per group, one lane per chunk.
 // Any other group (gaps, IP options, short packets) uses the row path.
 struct FlatGroup {
   int lo[4], hi[4], hole[4];  // positions relative to the aligned run base
@@ -119,6 +119,9 @@ __device__ __forceinline__ bool flat_group(uint8_t* __restrict__ arena, const wg
   }
   const int nch = (hi[3] + 15) >> 4;
   uint32_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
+  // clean chunks: all 16 bytes inside one packet's summed range (and, for
+  // L4_FILL, clear of its checksum field), summed unmasked with no divergent
+  // path; every other chunk contributes 0 here and is settled below
   for (int c0 = 0; c0 < nch; c0 += 64 * U) {  // wave-uniform
     uint4 v[U];
 #pragma unroll
@@ -126,64 +129,59 @@ __device__ __forceinline__ bool flat_group(uint8_t* __restrict__ arena, const wg
       const int c = c0 + 64 * u + lane;
       v[u] = c < nch ? ld_chunk<NT>(src + c) : make_uint4(0, 0, 0, 0);
     }
-    // dirty-chunk masks of this window (wave-uniform, scalar)
-    uint64_t dm[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) dm[u] = 0;
-    auto mark = [&](int chunk) {
-      const int rc = chunk - c0;
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (rc >= 64 * u && rc < 64 * u + 64) dm[u] |= 1ull << (rc - 64 * u);
-    };
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (lo[q] & 15) mark(lo[q] >> 4);
-      if (hi[q] & 15) mark(hi[q] >> 4);
-      if (MODE == WGCS_MODE_L4_FILL) {
-        mark(hole[q] >> 4);
-        mark((hole[q] + 1) >> 4);
-      }
-    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int c = c0 + 64 * u + lane;
-      const int x = 16 * c;
-      const int f = (x >= hi[0]) + (x >= hi[1]) + (x >= hi[2]);
-      if (((dm[u] >> lane) & 1ull) == 0) {
-        if (c < nch && x >= lo[0]) {  // clean chunk: all 16 bytes summed into packet f
-          const uint32_t t = add_halves(add_halves(add_halves(add_halves(0u, v[u].x), v[u].y), v[u].z), v[u].w);
-          acc0 += f == 0 ? t : 0u;
-          acc1 += f == 1 ? t : 0u;
-          acc2 += f == 2 ? t : 0u;
-          acc3 += f == 3 ? t : 0u;
-        }
-      } else {
-        // dirty: masked shares of packets f and f + 1 (a 16-byte chunk meets at most two ranges)
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int k = f + e;
-          if (k > 3) break;
-          const int klo = k == 0 ? lo[0] : (k == 1 ? lo[1] : (k == 2 ? lo[2] : lo[3]));
-          const int khi = k == 0 ? hi[0] : (k == 1 ? hi[1] : (k == 2 ? hi[2] : hi[3]));
-          const int kh = k == 0 ? hole[0] : (k == 1 ? hole[1] : (k == 2 ? hole[2] : hole[3]));
-          uint32_t m16 = byte_bits16(klo - x, khi - x);
-          if (MODE == WGCS_MODE_L4_FILL) m16 &= ~byte_bits16(kh - x, kh + 2 - x);
-          const uint32_t t = add_halves(add_halves(add_halves(add_halves(0u, v[u].x & expand_nibble(m16 & 0xFu)),
-                                                              v[u].y & expand_nibble((m16 >> 4) & 0xFu)),
-                                                   v[u].z & expand_nibble((m16 >> 8) & 0xFu)),
-                                        v[u].w & expand_nibble((m16 >> 12) & 0xFu));
-          acc0 += k == 0 ? t : 0u;
-          acc1 += k == 1 ? t : 0u;
-          acc2 += k == 2 ? t : 0u;
-          acc3 += k == 3 ? t : 0u;
-        }
+      const int x = 16 * (c0 + 64 * u + lane);
+      const bool b0 = x >= hi[0], b1 = x >= hi[1], b2 = x >= hi[2];  // packet f = b0 + b1 + b2
+      const int lo_f = b2 ? lo[3] : (b1 ? lo[2] : (b0 ? lo[1] : lo[0]));
+      const int hi_f = b2 ? hi[3] : (b1 ? hi[2] : (b0 ? hi[1] : hi[0]));
+      bool clean = x >= lo_f && x + 16 <= hi_f;  // also false past the run
+      if (MODE == WGCS_MODE_L4_FILL) {
+        const int h_f = b2 ? hole[3] : (b1 ? hole[2] : (b0 ? hole[1] : hole[0]));
+        clean = clean && (x >= h_f + 2 || x + 16 <= h_f);
       }
+      uint32_t t = add_halves(add_halves(add_halves(add_halves(0u, v[u].x), v[u].y), v[u].z), v[u].w);
+      t = clean ? t : 0u;
+      acc0 += b0 ? 0u : t;
+      acc1 += (b0 && !b1) ? t : 0u;
+      acc2 += (b1 && !b2) ? t : 0u;
+      acc3 += b2 ? t : 0u;
     }
     acc0 = fold32_16(acc0);
     acc1 = fold32_16(acc1);
     acc2 = fold32_16(acc2);
     acc3 = fold32_16(acc3);
+  }
+  // dirty chunks, once per group: lane 4q + s takes packet q's candidate s
+  // (its first chunk, its last chunk, the two chunks of its checksum field)
+  // unless an earlier candidate is the same chunk or the chunk is clean for q
+  // (counted above); its masked share of q goes into the lane's acc_q.  The
+  // chunk was just streamed, so the reload hits the cache.
+  {
+    const int q = (lane >> 2) & 3, sl = lane & 3;
+    const int lq = q == 0 ? lo[0] : (q == 1 ? lo[1] : (q == 2 ? lo[2] : lo[3]));
+    const int hq = q == 0 ? hi[0] : (q == 1 ? hi[1] : (q == 2 ? hi[2] : hi[3]));
+    const int hl = q == 0 ? hole[0] : (q == 1 ? hole[1] : (q == 2 ? hole[2] : hole[3]));
+    const int k0 = lq >> 4, k1 = (hq - 1) >> 4, k2 = hl >> 4, k3 = (hl + 1) >> 4;
+    const int cc = sl == 0 ? k0 : (sl == 1 ? k1 : (sl == 2 ? k2 : k3));
+    bool take = lane < 16 && (MODE == WGCS_MODE_L4_FILL || sl < 2);
+    take = take && !(sl >= 1 && cc == k0) && !(sl >= 2 && cc == k1) && !(sl == 3 && cc == k2);
+    const int x = 16 * cc;
+    bool clean = x >= lq && x + 16 <= hq;
+    if (MODE == WGCS_MODE_L4_FILL) clean = clean && (x >= hl + 2 || x + 16 <= hl);
+    if (take && !clean) {
+      const uint4 w = ld_chunk<false>(src + cc);
+      uint32_t m16 = byte_bits16(lq - x, hq - x);
+      if (MODE == WGCS_MODE_L4_FILL) m16 &= ~byte_bits16(hl - x, hl + 2 - x);
+      const uint32_t t = add_halves(add_halves(add_halves(add_halves(0u, w.x & expand_nibble(m16 & 0xFu)),
+                                                          w.y & expand_nibble((m16 >> 4) & 0xFu)),
+                                               w.z & expand_nibble((m16 >> 8) & 0xFu)),
+                                    w.w & expand_nibble((m16 >> 12) & 0xFu));
+      if (q == 0) acc0 = fold32_16(acc0 + t);
+      else if (q == 1) acc1 = fold32_16(acc1 + t);
+      else if (q == 2) acc2 = fold32_16(acc2 + t);
+      else acc3 = fold32_16(acc3 + t);
+    }
   }
   // per packet: wave sum, parity (pairing from the packet's first summed byte), pseudo-header constant
   uint32_t t4[4];
