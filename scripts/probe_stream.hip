@@ -236,3 +236,52 @@ extern "C" int probe_rowsg_launch(const void* src, const void* desc, uint32_t np
   } else { if (use_desc) RG(64, 2, true); else RG(64, 2, false); }
   return (int)hipGetLastError();
 }
+
+// Flat stream in items of ITEM_KB KiB per wave, each item preceded by a
+// dependent 16-byte "descriptor" load (the item's offset comes from it) and
+// closed by NRED wave reductions + one store per reduction: the per-group
+// prologue / epilogue of a per-packet kernel on top of the flat pattern.
+__device__ __forceinline__ uint32_t probe_wave_sum(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor((int)v, o);
+  return v;
+}
+template <int ITEM_KB, int NRED>
+__global__ __launch_bounds__(256) void probe_items(const uint4* __restrict__ src, size_t n16,
+                                                   const uint4* __restrict__ desc, uint32_t* __restrict__ out) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t nw = gridDim.x * 4;
+  const int lane = threadIdx.x & 63;
+  const size_t n_items = n16 / (64 * ITEM_KB);
+  for (size_t it = wave; it < n_items; it += nw) {
+    const uint4 d = desc[it];  // dependent: the item's chunk base comes from memory
+    const size_t b = ((size_t)d.y << 32) | d.x;
+    uint32_t acc[NRED];
+#pragma unroll
+    for (int q = 0; q < NRED; ++q) acc[q] = 0;
+#pragma unroll
+    for (int k0 = 0; k0 < ITEM_KB; k0 += 4) {
+      u4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = k0 + u < ITEM_KB ? __builtin_nontemporal_load((const u4*)(src + b + (k0 + u) * 64 + lane)) : u4{0, 0, 0, 0};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[(k0 + u) % NRED] += v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+#pragma unroll
+    for (int q = 0; q < NRED; ++q) {
+      const uint32_t s = probe_wave_sum(acc[q]);
+      if (lane == q) out[it * NRED + q] = s;
+    }
+  }
+}
+extern "C" int probe_items_launch(const void* src, size_t bytes, const void* desc, void* out, int grid, int item_kb,
+                                  void* stream) {
+  const size_t n16 = bytes / 16;
+  hipStream_t s = (hipStream_t)stream;
+#define PI(K, R) hipLaunchKernelGGL((probe_items<K, R>), dim3(grid), dim3(256), 0, s, (const uint4*)src, n16, (const uint4*)desc, (uint32_t*)out)
+  if (item_kb == 6) PI(6, 4);
+  else if (item_kb == 12) PI(12, 8);
+  else PI(24, 16);
+  return (int)hipGetLastError();
+}
