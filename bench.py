@@ -69,13 +69,22 @@ def main():
 
     world, rank, local = shard.dist_env()
     dist = None
+    # WGCS_DIST_BACKEND=gloo rehearses the N>1 bench on a box with fewer GPUs
+    # than ranks (ranks then share devices round-robin); the driver's runs use
+    # RCCL ("nccl") with one GPU per rank.
+    backend = os.environ.get("WGCS_DIST_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
 
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
+    red_dev = "cuda" if backend == "nccl" else "cpu"
 
     def barrier():
         if dist is not None:
@@ -147,7 +156,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / args.steps if use_events else None
-    elapsed = shard.max_over_ranks(elapsed, dist, device="cuda")
+    elapsed = shard.max_over_ranks(elapsed, dist, device=red_dev)
 
     total_bytes = bytes_per_step * args.steps * world  # every rank processed bytes_per_step per step
     if scaling == "strong":

@@ -17,7 +17,7 @@ import time
 
 import numpy as np
 
-from . import synth
+from . import shard, synth
 
 OFFSET = 16
 CAP = 65535 + OFFSET
@@ -90,10 +90,7 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
         call()
         t_total += time.perf_counter() - t0
     barrier()
-    if dist is not None:
-        t = torch.tensor([t_total], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_total = float(t.item())
+    t_total = shard.max_over_ranks(t_total, dist)
     per = t_total / args.steps
     result = {
         "metric": "Tun.Write handleGRO packets/s (host buffers, 128-packet batch)",

@@ -13,7 +13,7 @@ import time
 
 import numpy as np
 
-from . import synth
+from . import shard, synth
 from .tun import GSO_JOB_DTYPE
 
 HBM_PEAK_GBS = 8000.0
@@ -65,10 +65,7 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / args.steps
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(elapsed, dist)
     achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
     # calibration: a plain device-to-device copy of the super-packet bytes
     # (same read + write volume, same rotation) with the runtime's copy kernel

@@ -66,6 +66,8 @@ def max_over_ranks(value: float, dist, device=None) -> float:
         return value
     import torch
 
+    if device is None:  # RCCL reduces device tensors; gloo (CPU tests, rehearsals) host tensors
+        device = "cuda" if dist.get_backend() == "nccl" else "cpu"
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

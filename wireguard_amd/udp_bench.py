@@ -18,7 +18,7 @@ import time
 
 import numpy as np
 
-from . import synth
+from . import shard, synth
 
 HBM_PEAK_GBS = 8000.0
 MSG = 1452  # transport message for a 1420-B tunnel MTU: 16-B header + 1420 + 16-B tag
@@ -81,12 +81,7 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
         res = run_split(args, torch, dev, rank, world, barrier)
     else:
         res = run_coalesce(args, torch, dev, rank, world, barrier)
-    if dist is not None:
-        t = torch.tensor([res.pop("_elapsed")], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    else:
-        elapsed = res.pop("_elapsed")
+    elapsed = shard.max_over_ranks(res.pop("_elapsed"), dist)
     bps = res["roofline"]["algorithmic_bytes_per_launch"]
     res["value"] = round(bps * args.steps * world / elapsed / 2**30, 2)
     res["ms_per_step"] = round(elapsed / args.steps * 1e3, 5)
