@@ -426,6 +426,7 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   Job jd = {};
   bool jd_ok = false;
   if (wv == kDec) {
+    __builtin_amdgcn_s_setprio(3);  // the decode chain is the block's critical path (until barrier 2)
     hb.load(vb, (int)min(jlen, 256u), lane);
 #if WGCS_GSO_EXP & 64
     if (__builtin_amdgcn_readfirstlane((int)(hb.r0 + hb.r3)) == -1) hb.r1 = 0;  // stamp 5: header bytes arrived
@@ -498,11 +499,15 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   const int hph_s = (int)((uintptr_t)rb & 15u);
   const uint8_t* hab_s = rb - hph_s + 16 * r;
   const uint8_t* hend_s = rb + min(plen_s, kMaxHdrLen + 16);
-  uint4 H0 = z, H1 = z;
-  if (spec) {
-    if (hab_s < hend_s) H0 = ld16(hab_s);
-    if (hab_s + 16 < hend_s) H1 = ld16(hab_s + 16);
-  }
+  // Issued unconditionally, only the address is selected (a chunk past
+  // hend_s reads the chunk holding rb, a row that does not speculate reads
+  // the job table; the fast path uses H0/H1 only when spec_ok and never their
+  // bytes past hdrLen).  Together with the decoder's raised priority: 11.74 ->
+  // 11.54 us on cfg4 (each change alone was slower, scripts/exp_gso.sh).
+  const uint8_t* hsafe = rb - hph_s;  // the 16-byte chunk holding rb
+  const uint8_t* hdummy = reinterpret_cast<const uint8_t*>(jobs);
+  uint4 H0 = ld_src<NT>(spec ? (hab_s < hend_s ? hab_s : hsafe) : hdummy);
+  uint4 H1 = ld_src<NT>(spec ? (hab_s + 16 < hend_s ? hab_s + 16 : hsafe) : hdummy);
 
   lds_barrier();  // barrier 1: geometry; the speculative loads stay in flight
   GSO_STAMP(1);
@@ -528,6 +533,7 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
     // for: s_barrier only counts the workgroup's surviving waves.
     lds_barrier();
   }
+  if (wv == kDec) __builtin_amdgcn_s_setprio(0);
   Job j = {};
   j.status = ufl(ji.status);
   j.nseg = ufl(ji.nseg);
