@@ -33,7 +33,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
 CONFIGS = {
     # name: (packets, frame_len, kinds, BASELINE.json configs index, scaling)
@@ -64,7 +63,7 @@ def main():
     args = parse()
     import torch  # before wireguard_amd: one HIP runtime per process
 
-    from wireguard_amd import shard, synth
+    from wireguard_amd import shard, synth, traffic
     from wireguard_amd.tun import Device, MODE_VALIDATE, MODE_L4_FILL
 
     world, rank, local = shard.dist_env()
@@ -196,7 +195,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic_per_launch(kname, bytes_per_step),
+            "traffic": traffic.per_launch(kname, bytes_per_step),
             "kernel": kname,
             "kernel_ms": round(kern_ms, 5),
             "algorithmic_bytes_per_launch": bytes_per_step,
@@ -227,21 +226,6 @@ def _tune_tag():
     else:
         g, u = 16, (8 if u >= 8 else (6 if u >= 6 else 4))
     return f"{g},{u}"
-
-
-def traffic_per_launch(kname, algo_bytes):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass
-    (profiles/traffic.json, written by scripts/pmc_traffic.py from
-    FETCH_SIZE x 2 x 1024 + WRITE_SIZE x 1024, MI355X_MICROARCH.md §HBM)."""
-    try:
-        with open(TRAFFIC_FILE) as f:
-            t = json.load(f)
-        rec = t.get(kname)
-        if rec and rec.get("algorithmic_bytes") == algo_bytes:
-            return rec["hbm_bytes_per_launch"]
-    except (OSError, ValueError):
-        pass
-    return None
 
 
 def end_to_end(torch, dev, arena_np, pkts_np, mode, stream, iters=20):

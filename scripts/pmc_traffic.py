@@ -1,14 +1,16 @@
-"""Per-launch HBM traffic of the checksum kernel from rocprofv3 PMC passes.
+"""Per-launch HBM traffic of the path's kernels from rocprofv3 PMC passes.
 
-usage: python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR ALGO_BYTES [out.json]
+usage: python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR ALGO_BYTES [KERNEL_SUBSTR] [out.json]
 
 FETCH_DIR / WRITE_DIR: `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE`
-output directories (separate passes: FETCH_SIZE costs 3 TCC slots, WRITE_SIZE
-2; MI355X_MICROARCH.md §rocprofv3 PMC slots).  Correction per the guide
-(§HBM): FETCH_SIZE is in KiB and reads exactly 1/2 of a wide coalesced
-stream's bytes on gfx950, so hbm_read = FETCH_SIZE x 1024 x 2;
-hbm_write = WRITE_SIZE x 1024.  Writes profiles/traffic.json, which bench.py
-reports as roofline.traffic.
+output directories of the same bench command (separate passes: FETCH_SIZE
+costs 3 TCC slots, WRITE_SIZE 2; MI355X_MICROARCH.md §rocprofv3 PMC slots).
+Correction per the guide (§HBM): FETCH_SIZE is in KiB and reads exactly 1/2
+of a wide coalesced stream's bytes on gfx950, so hbm_read = FETCH_SIZE x 1024
+x 2; hbm_write = WRITE_SIZE x 1024.  KERNEL_SUBSTR (default
+checksum_batch_kernel) picks the kernel; its record is merged into
+profiles/traffic.json under the name the bench line reports
+(wireguard_amd/traffic.py reads it back).
 """
 import csv
 import glob
@@ -19,34 +21,55 @@ import statistics
 import sys
 
 
-def counter(d, name):
+def counter(d, name, sub):
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == name and "checksum_batch_kernel" in r["Kernel_Name"]:
+            if r["Counter_Name"] == name and sub in r["Kernel_Name"]:
                 vals.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     return vals
 
 
+def bench_key(k):
+    """The kernel name as bench.py / gso_bench / udp_bench report it."""
+    m = re.search(r"checksum_batch_kernel<(\d+), (\d+), (\d+), (true|false)", k)
+    if m:
+        mode = {"2": "VALIDATE", "1": "L4_FILL"}.get(m.group(1), m.group(1))
+        return f"checksum_batch_kernel<{mode},{m.group(2)},{m.group(3)},{'nt' if m.group(4) == 'true' else 'rt'}>"
+    m = re.search(r"gso_rows_kernel<(\d+), (true|false)>", k)
+    if m:
+        return f"gso_rows_kernel<{m.group(1)},{m.group(2)}>"
+    m = re.search(r"udp_split_kernel<(\d+)>", k)
+    if m:
+        return f"udp_split_kernel<{m.group(1)}>"
+    m = re.search(r"udp_coalesce_kernel<(\d+), (\d+)>", k)
+    if m:
+        return f"udp_coalesce_kernel<{m.group(1)},{m.group(2)}>"
+    return k
+
+
 def main():
     fdir, wdir, algo = sys.argv[1], sys.argv[2], int(sys.argv[3])
-    out = sys.argv[4] if len(sys.argv) > 4 else os.path.join(os.path.dirname(os.path.dirname(
+    sub = sys.argv[4] if len(sys.argv) > 4 else "checksum_batch_kernel"
+    out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(os.path.dirname(
         os.path.abspath(__file__))), "profiles", "traffic.json")
-    fs, ws = counter(fdir, "FETCH_SIZE"), counter(wdir, "WRITE_SIZE")
-    res = {}
+    fs, ws = counter(fdir, "FETCH_SIZE", sub), counter(wdir, "WRITE_SIZE", sub)
+    try:
+        with open(out) as f:
+            res = json.load(f)
+    except (OSError, ValueError):
+        res = {}
     for k, v in fs.items():
-        targs = re.search(r"checksum_batch_kernel<(\d+), (\d+), (\d+), (true|false)>", k)
-        mode = {"2": "VALIDATE", "1": "L4_FILL"}.get(targs.group(1), targs.group(1))
-        key = f"checksum_batch_kernel<{mode},{targs.group(2)},{targs.group(3)},{'nt' if targs.group(4) == 'true' else 'rt'}>"
         rd = statistics.median(v) * 1024 * 2
         wr = statistics.median(ws.get(k, [0.0])) * 1024
-        res[key] = {"hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
-                    "algorithmic_bytes": algo, "launches": len(v), "kernel": k,
-                    "method": "median FETCH_SIZE x1024 x2 (gfx950 half-count) + WRITE_SIZE x1024, separate passes",
-                    "source_dirs": [fdir, wdir]}
+        res[bench_key(k)] = {"hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
+                             "algorithmic_bytes": algo, "launches": len(v), "kernel": k,
+                             "method": "median FETCH_SIZE x1024 x2 (gfx950 half-count) + WRITE_SIZE x1024, "
+                                       "separate passes",
+                             "source_dirs": [fdir, wdir]}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
-    print(json.dumps(res, indent=1))
+    print(json.dumps({k: res[k] for k in map(bench_key, fs)}, indent=1))
 
 
 if __name__ == "__main__":

@@ -13,7 +13,7 @@ import time
 
 import numpy as np
 
-from . import shard, synth
+from . import shard, synth, traffic
 from .tun import GSO_JOB_DTYPE
 
 HBM_PEAK_GBS = 8000.0
@@ -108,7 +108,7 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": traffic.per_launch("gso_rows_kernel<6,true>", bytes_per_step),
             "kernel": "gso_rows_kernel<6,true>",
             "kernel_ms": round(kern_ms, 5),
             "algorithmic_bytes_per_launch": bytes_per_step,

@@ -1,0 +1,26 @@
+"""Per-launch HBM traffic of the path's kernels, as the bench lines report it
+(roofline.traffic): read from the committed profiles/traffic.json, which
+scripts/pmc_traffic.py writes from separate rocprofv3 FETCH_SIZE / WRITE_SIZE
+passes (FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024 on gfx950,
+MI355X_MICROARCH.md §HBM).  Bench-side bookkeeping only, not the data path."""
+from __future__ import annotations
+
+import json
+import os
+
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                            "traffic.json")
+
+
+def per_launch(kname: str, algo_bytes: int):
+    """HBM bytes per launch of kernel `kname` for a launch of `algo_bytes`
+    algorithmic bytes, or None when no matching PMC record is committed."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    rec = t.get(kname)
+    if rec and rec.get("algorithmic_bytes") == algo_bytes:
+        return rec["hbm_bytes_per_launch"]
+    return None

@@ -18,7 +18,7 @@ import time
 
 import numpy as np
 
-from . import shard, synth
+from . import shard, synth, traffic
 
 HBM_PEAK_GBS = 8000.0
 MSG = 1452  # transport message for a 1420-B tunnel MTU: 16-B header + 1420 + 16-B tag
@@ -101,7 +101,7 @@ def _result(metric, args, workload, extra, kname, kern_ms, bps, copy_ms, elapsed
         "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic", "config": {"workload": workload, **extra},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic.per_launch(kname, bps), "kernel": kname,
                      "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_launch": bps,
                      "d2d_copy_same_bytes_ms": round(copy_ms, 5)},
         "_elapsed": elapsed,
