@@ -174,3 +174,45 @@ def test_reference_shaped_single_calls(dev):
     assert dev.gso_none_checksum(rb, 21, 16) is None
     oracle.lib().or_gso_none_checksum((np.frombuffer(rb2, np.uint8)).ctypes.data, len(rb2), 21, 16)
     assert rb == rb2
+
+
+@pytest.fixture(scope="module")
+def flat_dev():
+    """A context launched with the opt-in flat-group mapping (16-lane rows,
+    4 back-to-back frames streamed as one run)."""
+    import os
+
+    from wireguard_amd.tun import Device
+
+    keys = ("WGCS_LANES_PER_PKT", "WGCS_FLAT", "WGCS_UNROLL")
+    old = {k: os.environ.get(k) for k in keys}
+    os.environ.update({"WGCS_LANES_PER_PKT": "16", "WGCS_FLAT": "1", "WGCS_UNROLL": "4"})
+    try:
+        d = Device(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    yield d
+    d.close()
+
+
+@pytest.mark.parametrize("kinds", ["tcp4", "udp4", "tcp6", "mixed"])
+@pytest.mark.parametrize("frame_len,stride", [(1500, None), (1501, None), (1499, None), (9000, None), (300, None),
+                                              (1500, 1504), (61, None)])
+@pytest.mark.parametrize("valid", [True, False])
+def test_flat_group_path(flat_dev, kinds, frame_len, stride, valid):
+    """Back-to-back groups take the flat stream (clean chunks branch-free,
+    dirty chunks settled once per group); gaps (stride), IPv6-in-mixed groups
+    and short frames exercise its fallback to the row path."""
+    arena, pkts, _ = synth.make_batch(1027, frame_len, kinds=kinds, stride=stride, valid=valid,
+                                      seed=frame_len + len(kinds))
+    got, want, _, _ = _both(flat_dev, MODE_VALIDATE, arena, pkts)
+    assert np.array_equal(got, want)
+    assert bool(got.all()) == valid
+    got, want, _, _ = _both(flat_dev, MODE_L4_FILL, arena, pkts)
+    assert np.array_equal(got, want)
+    got, want, ag, ac = _both(flat_dev, MODE_L4_FILL, arena, pkts, inplace=True)
+    assert np.array_equal(got, want) and np.array_equal(ag, ac)
