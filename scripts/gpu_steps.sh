@@ -48,6 +48,7 @@ for s in "$@"; do
     pmc-w) (cd /tmp && step pmcw 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e --no-event-timing) ;;
     prof-cfg4) (cd /tmp && step prof_cfg4 400 rocprofv3 --kernel-trace --stats -d "$OUT/profcfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e) ;;
     pmc-gso) (cd /tmp && step pmcf_cfg4 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_cfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 30 --warmup 3 --cpu-seconds 0 --no-e2e) && (cd /tmp && step pmcw_cfg4 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_cfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 30 --warmup 3 --cpu-seconds 0 --no-e2e) ;;
+    pmc-cs) for c in "cfg2 --mode fill" "cfg3" "cfg5"; do t=$(echo $c | tr -d ' -'); (cd /tmp && step pmcf_$t 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_${t}_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config $c --steps 30 --warmup 3 --cpu-seconds 0 --no-e2e --no-event-timing) && (cd /tmp && step pmcw_$t 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_${t}_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config $c --steps 30 --warmup 3 --cpu-seconds 0 --no-e2e --no-event-timing) || exit 1; done ;;
     pmc-udp) for c in udp_split udp_coalesce; do (cd /tmp && step pmcf_$c 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_${c}_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config $c --steps 20 --warmup 3 --cpu-seconds 0 --no-e2e) && (cd /tmp && step pmcw_$c 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_${c}_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config $c --steps 20 --warmup 3 --cpu-seconds 0 --no-e2e) || exit 1; done ;;
     pmc-sq-cfg4) (cd /tmp && step pmcsq_cfg4 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace -d "$OUT/pmcsqcfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 20 --warmup 2 --cpu-seconds 0) ;;
     pmc-sq2-cfg4) (cd /tmp && step pmcsq2_cfg4 400 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcsq2cfg4_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 20 --warmup 2 --cpu-seconds 0) ;;

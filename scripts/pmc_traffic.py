@@ -59,17 +59,24 @@ def main():
             res = json.load(f)
     except (OSError, ValueError):
         res = {}
+    new = {}
     for k, v in fs.items():
         rd = statistics.median(v) * 1024 * 2
         wr = statistics.median(ws.get(k, [0.0])) * 1024
-        res[bench_key(k)] = {"hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
-                             "algorithmic_bytes": algo, "launches": len(v), "kernel": k,
-                             "method": "median FETCH_SIZE x1024 x2 (gfx950 half-count) + WRITE_SIZE x1024, "
-                                       "separate passes",
-                             "source_dirs": [fdir, wdir]}
+        rec = {"hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
+               "algorithmic_bytes": algo, "launches": len(v), "kernel": k,
+               "method": "median FETCH_SIZE x1024 x2 (gfx950 half-count) + WRITE_SIZE x1024, separate passes",
+               "source_dirs": [fdir, wdir]}
+        key = bench_key(k)
+        # one record per (kernel, launch size): a list once a kernel has several
+        old = res.get(key)
+        old = old if isinstance(old, list) else ([old] if old else [])
+        old = [r for r in old if r.get("algorithmic_bytes") != algo] + [rec]
+        res[key] = old[0] if len(old) == 1 else old
+        new[key] = rec
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
-    print(json.dumps({k: res[k] for k in map(bench_key, fs)}, indent=1))
+    print(json.dumps(new, indent=1))
 
 
 if __name__ == "__main__":

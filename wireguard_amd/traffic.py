@@ -20,7 +20,8 @@ def per_launch(kname: str, algo_bytes: int):
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    rec = t.get(kname)
-    if rec and rec.get("algorithmic_bytes") == algo_bytes:
-        return rec["hbm_bytes_per_launch"]
+    recs = t.get(kname)
+    for rec in (recs if isinstance(recs, list) else [recs]):  # one record per launch size
+        if rec and rec.get("algorithmic_bytes") == algo_bytes:
+            return rec["hbm_bytes_per_launch"]
     return None
