@@ -391,6 +391,8 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
                                                         uint32_t offset, uint32_t room, int32_t* __restrict__ sizes,
                                                         int32_t* __restrict__ count, int32_t* __restrict__ status) {
   __shared__ JobInfo ji;
+  __shared__ uint32_t s_tpay[64];   // per segment of the block: row-reduced payload sum (dense header phase)
+  __shared__ uint4 s_keep[64][8];   // per segment: payload bytes of destination chunks 0..7
   const int lane = threadIdx.x & 63;
   const int r = lane & 15;
   const int wv = threadIdx.x >> 6;
@@ -612,12 +614,94 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   }
   GSO_STAMP(3);
 
+  // ---- lane-dense header phase (fast headers of <= 113 bytes): the row
+  // publishes its payload sum and the payload part of its header chunks, and
+  // after barrier 2 Ld = 4 or 8 lanes per segment (instead of a whole 16-lane
+  // row, of which only hk lanes hold header bytes) rewrite and store the
+  // headers: 16 or 8 segments per wave, a quarter or half of the VALU issue.
+  // Block-uniform; needs the decoder wave to own no segment of this block
+  // (its rows publish only after barrier 2).
+  const int nb = min(64, j.nseg - (int)(blockIdx.y * 64u));
+  const int Ld = nb <= 60 ? (hdr_len <= 49 ? 4 : (hdr_len <= 113 ? 8 : 0)) : 0;
+  if (Ld) {
+    const uint32_t tp = fold32_16(row16_sum_u32(acc));
+    const int sloc_r = i - (int)(blockIdx.y * 64u);
+    if (r == 0) s_tpay[sloc_r] = tp;
+    if (r < 8) s_keep[sloc_r][r] = keep;
+  }
+
   // ---- job-constant header sums (barrier 2; the decoder wave passed it already)
   if (wv != kDec) lds_barrier();
   const bool fast = ufl(ji.fast) != 0;
   const uint32_t id0 = (uint32_t)ufl((int)ji.id0), seq0 = (uint32_t)ufl((int)ji.seq0);
   const uint32_t ip_base = (uint32_t)ufl((int)ji.ip_base), l4_base = (uint32_t)ufl((int)ji.l4_base);
   const uint32_t addr_sum = (uint32_t)ufl((int)ji.addr), tflags = (uint32_t)ufl((int)ji.tflags);
+
+  if (fast && Ld) {
+    const int spw = 64 / Ld;                   // segments per wave
+    if (wv * spw >= nb) return;                // wave-uniform: no header of this wave
+    const int sl = lane / Ld, c = lane % Ld;   // segment within the wave, header chunk
+    const int sloc = wv * spw + sl;
+    const bool valid2 = sloc < nb;             // lanes of live rows (Ld <= 16)
+    const int i2 = (int)(blockIdx.y * 64u) + (valid2 ? sloc : 0);
+    const int seg_start2 = hdr_len + i2 * j.gso;
+    const int seg_end2 = min(plen, seg_start2 + j.gso);
+    const int seg_len2 = seg_end2 - seg_start2;
+    const int pkt_len2 = hdr_len + seg_len2;
+    const bool last2 = seg_end2 == plen;
+    uint8_t* dst2 = out + obase + (uint64_t)i2 * opitch + offset;
+    const int dalign2 = (int)((uintptr_t)dst2 & 15u);
+    uint8_t* dbase2 = dst2 - dalign2;
+    const int nk2 = (pkt_len2 + dalign2 + 15) >> 4;
+    const int hk2 = min((hdr_len + dalign2 + 15) >> 4, nk2);
+    // header source chunks c, c + 1 (packet coordinates, wave-uniform phase):
+    // the speculative H0/H1 of this wave's first row, lane c (its segment
+    // speculated: it is live), fetched across lanes -- no memory round trip
+    // after the barrier.  Their bytes past hdrLen are never used.
+    const int hph = (int)((uintptr_t)rb & 15u);
+    const uint4 G0 = make_uint4((uint32_t)__shfl((int)H0.x, c), (uint32_t)__shfl((int)H0.y, c),
+                                (uint32_t)__shfl((int)H0.z, c), (uint32_t)__shfl((int)H0.w, c));
+    const uint4 G1 = make_uint4((uint32_t)__shfl((int)H1.x, c), (uint32_t)__shfl((int)H1.y, c),
+                                (uint32_t)__shfl((int)H1.z, c), (uint32_t)__shfl((int)H1.w, c));
+    const uint32_t id = i2 > 0 ? ((id0 + 1) & 0xFFFFu) : id0;  // quirk: id0 + 1 for every i >= 1 (:1426-1431)
+    const uint32_t seq = seq0 + (uint32_t)(uint16_t)((uint16_t)j.gso * (uint16_t)i2);  // uint16 product (:1445)
+    const uint32_t ulen = (uint32_t)(uint16_t)(seg_len2 + (hdr_len - cs));            // UDP length (:1462-1465)
+    const uint32_t tlen = (uint32_t)(uint16_t)(hdr_len - cs + seg_len2);              // transportLen (:1469-1471)
+    const uint32_t proto = tcp ? 6u : 17u;
+    uint32_t t_pay = s_tpay[valid2 ? sloc : 0];
+    if ((((uintptr_t)dst2 + (uintptr_t)cs) & 1u) == 0) t_pay = bswap16(t_pay);  // pairing from csumStart
+    const uint32_t var = tcp ? (seq >> 16) + (seq & 0xFFFFu) + (last2 ? (tflags & 0x09u) : 0u) : ulen;
+    const uint32_t l4c = (~fold32_16(t_pay + fold32_16(l4_base) + var + fold32_16(addr_sum) + proto + tlen)) & 0xFFFFu;
+    uint4 P = funnel(G0, G1, hph);
+    if (v4) {
+      const uint32_t ipc = (~fold32_16(fold32_16(ip_base) + (uint32_t)pkt_len2 + id)) & 0xFFFFu;
+      put_be16_u(P, c, 2, (uint32_t)pkt_len2);  // total length (:1433)
+      put_be16_u(P, c, 4, id);                  // identification (:1426-1431)
+      put_be16_u(P, c, 10, ipc);                // header checksum (:1434-1436)
+    } else {
+      put_be16_u(P, c, 4, (uint32_t)(pkt_len2 - cs));  // payload length (:1439)
+    }
+    if (tcp) {
+      put_be16_u(P, c, cs + 4, seq >> 16);  // sequence number (:1445-1446)
+      put_be16_u(P, c, cs + 6, seq);
+      put_u(P, c, cs + 13, last2 ? tflags : (tflags & ~0x09u), 0xFFu);  // FIN|PSH on the last only (:1447-1459)
+    } else {
+      put_be16_u(P, c, cs + 4, ulen);
+    }
+    put_be16_u(P, c, csum_at, l4c);  // L4 checksum (:1486-1490)
+    // to the destination phase: the previous chunk of the same segment (DPP
+    // row_shr:1; a group's first lane has none), merged with the payload bytes
+    uint4 Pp = row_prev4(P);
+    if (c == 0) Pp = z;
+    const uint4 D = dalign2 ? funnel_v(Pp, P, 16 - dalign2) : P;
+    const int x0h2 = 16 * c - dalign2;
+    const uint32_t hmask2 = byte_bits16(-x0h2, hdr_len - x0h2);
+    const uint4 keep2 = s_keep[valid2 ? sloc : 0][c];
+    if (valid2 && c < hk2) store_chunk(dbase2 + 16 * c, select_bytes(D, keep2, hmask2), x0h2, pkt_len2);
+    if (valid2 && c == 0) sizes[slot0 + (uint32_t)i2] = pkt_len2;
+    GSO_STAMP(4);
+    return;
+  }
 
   // ---- header source chunks (shared by the job's segments: L2 hits).
   // fast: packet coordinates (lane r = readBuf[16r, 16r + 16), wave-uniform
