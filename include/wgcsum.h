@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define WGCS_ABI_VERSION 1
+#define WGCS_ABI_VERSION 2 /* 2: wgcs_pkt carries proto and a u16 csum_offset */
 
 /* ---- status codes (negative); Go sentinel / error each one maps to ---- */
 #define WGCS_OK 0
@@ -65,17 +65,33 @@ extern "C" {
 #define WGCS_ERR_NOMEM (-101)
 #define WGCS_ERR_NO_DEVICE (-102)
 
-/* ---- batch descriptor: one packet (or byte range) in a device arena ---- */
+/* ---- batch descriptor: one packet (or byte range) in a device arena ----
+ * 16 bytes, loaded by the kernels as one dwordx4.  The arena offset is 48 bits
+ * (off_lo | off_hi << 32); the checksum field sits at the uint16 position
+ * (csum_start + csum_offset) & 0xFFFF, as the reference computes it
+ * (gro.go:1391, :1503).  wgcs_pkt_set() fills one. */
 typedef struct wgcs_pkt {
-  uint64_t off;        /* byte offset of the packet (IP header) in the arena      */
-  uint32_t len;        /* packet length in bytes (< 2^31)                           */
-  uint16_t csum_start; /* L4 start = IP header length (iphLen / virtio csumStart)   */
-  uint8_t csum_offset; /* checksum field offset from csum_start (16 TCP, 6 UDP)     */
-  uint8_t flags;       /* WGCS_PKT_*                                                */
-} wgcs_pkt;          /* 16 bytes */
+  uint32_t off_lo;      /* byte offset of the packet (IP header) in the arena, bits 0-31 */
+  uint16_t off_hi;      /* bits 32-47                                                    */
+  uint8_t proto;        /* pseudo-header protocol (checksumValid's `protocol`, any u8)   */
+  uint8_t flags;        /* WGCS_PKT_*                                                    */
+  uint32_t len;         /* packet length in bytes (< 2^31)                               */
+  uint16_t csum_start;  /* L4 start = IP header length (iphLen / virtio csumStart)       */
+  uint16_t csum_offset; /* checksum field offset from csum_start (16 TCP, 6 UDP, any)    */
+} wgcs_pkt;
 
-#define WGCS_PKT_V6 0x01  /* addresses at 8/24 (16 B) instead of 12/16 (4 B)         */
-#define WGCS_PKT_UDP 0x02 /* pseudo-header protocol 17 instead of 6                   */
+#define WGCS_PKT_V6 0x01 /* isV6: addresses at 8/24 (16 B) instead of 12/16 (4 B) */
+
+static inline void wgcs_pkt_set(wgcs_pkt *p, uint64_t off, uint32_t len, uint16_t csum_start,
+                                uint16_t csum_offset, uint8_t proto, uint8_t flags) {
+  p->off_lo = (uint32_t)off;
+  p->off_hi = (uint16_t)(off >> 32);
+  p->proto = proto;
+  p->flags = flags;
+  p->len = len;
+  p->csum_start = csum_start;
+  p->csum_offset = csum_offset;
+}
 
 /* ---- batch modes (out element: u16, except VALIDATE: u8 0/1) ---- */
 #define WGCS_MODE_FOLD 0     /* out = checksum(pkt[0:len], initial[i])                 checksum.go:152 */

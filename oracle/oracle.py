@@ -21,8 +21,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _SO = os.path.join(_HERE, "_build", "libwgoracle.so")
 
-PKT_DTYPE = np.dtype(
-    [("off", "<u8"), ("len", "<u4"), ("csum_start", "<u2"), ("csum_offset", "u1"), ("flags", "u1")]
+PKT_DTYPE = np.dtype(  # or_pkt == wgcs_pkt layout (ABI 2)
+    [("off_lo", "<u4"), ("off_hi", "<u2"), ("proto", "u1"), ("flags", "u1"), ("len", "<u4"),
+     ("csum_start", "<u2"), ("csum_offset", "<u2")]
 )
 assert PKT_DTYPE.itemsize == 16
 
@@ -131,6 +132,31 @@ def handle_virtio_read(read_buf: bytearray, bufs: list, offset: int):
     sizes = (C.c_int * len(bufs))()
     n = C.c_int(0)
     rc = lib().or_handle_virtio_read(_ptr(rb), len(rb), _bufs_ctypes(bufs), lens, len(bufs), sizes, offset, C.byref(n))
+    return rc, n.value, list(sizes)
+
+
+class VirtioHdr(C.Structure):  # or_virtio_hdr (gro.go:42-67)
+    _fields_ = [("flags", C.c_uint8), ("gso_type", C.c_uint8), ("hdr_len", C.c_uint16), ("gso_size", C.c_uint16),
+                ("csum_start", C.c_uint16), ("csum_offset", C.c_uint16)]
+
+
+def gso_split(read_buf, hdr: tuple, bufs: list, offset: int, is_v6: bool):
+    """Oracle gsoSplit(readBuf, hdr, bufs, sizes, offset, isV6).  hdr =
+    (flags, gso_type, hdr_len, gso_size, csum_start, csum_offset).  Mutates
+    read_buf and bufs.  Returns (rc, n, sizes)."""
+    L = lib()
+    if not getattr(L, "_split_ready", False):
+        u8p = C.POINTER(C.c_uint8)
+        L.or_gso_split.argtypes = [C.c_void_p, C.c_size_t, VirtioHdr, C.POINTER(u8p), C.POINTER(C.c_size_t), C.c_int,
+                                   C.POINTER(C.c_int), C.c_int, C.c_int, C.POINTER(C.c_int)]
+        L.or_gso_split.restype = C.c_int
+        L._split_ready = True
+    rb = np.frombuffer(read_buf, dtype=np.uint8) if not isinstance(read_buf, np.ndarray) else read_buf
+    lens = (C.c_size_t * len(bufs))(*[len(b) for b in bufs])
+    sizes = (C.c_int * len(bufs))()
+    n = C.c_int(0)
+    rc = L.or_gso_split(_ptr(rb) if len(rb) else None, len(rb), VirtioHdr(*hdr), _bufs_ctypes(bufs), lens, len(bufs),
+                        sizes, offset, int(is_v6), C.byref(n))
     return rc, n.value, list(sizes)
 
 

@@ -121,8 +121,8 @@ enum { VNET_LEN = 10, F_NEEDS_CSUM = 1, GSO_NONE = 0, GSO_TCPV4 = 1, GSO_TCPV6 =
 enum { TCP_FLAGS_OFF = 13, TCP_FIN = 0x01, TCP_PSH = 0x08, TCP_ACK = 0x10, UDPH_LEN = 8 };
 
 /* gro.go:554-612 */
-int or_checksum_valid(const uint8_t *pkt, size_t len, uint8_t iph_len,
-                      uint8_t proto, int is_v6) {
+static int checksum_valid_at(const uint8_t *pkt, size_t len, size_t iph_len,
+                             uint8_t proto, int is_v6) {
   size_t src_at = is_v6 ? IPV6_SRC : IPV4_SRC;
   size_t addr = is_v6 ? 16 : 4;
   if (len < src_at + 2 * addr || len < iph_len) return 0; /* would panic */
@@ -130,6 +130,10 @@ int or_checksum_valid(const uint8_t *pkt, size_t len, uint8_t iph_len,
   uint64_t ph = or_pseudo_header_nofold(pkt + src_at, pkt + src_at + addr, addr,
                                         proto, total_len);
   return (uint16_t)~or_checksum(pkt + iph_len, len - iph_len, ph) == 0;
+}
+int or_checksum_valid(const uint8_t *pkt, size_t len, uint8_t iph_len,
+                      uint8_t proto, int is_v6) {
+  return checksum_valid_at(pkt, len, iph_len, proto, is_v6);
 }
 
 /* gro.go:1497-1517 */
@@ -143,34 +147,43 @@ int or_gso_none_checksum(uint8_t *rb, size_t len, uint16_t csum_start,
   return OR_OK;
 }
 
-/* gro.go:1373-1493 */
+/* gro.go:1373-1493.  Every index the reference computes from hdr fields is a
+ * uint16 sum (hdr.csumStart+4, +tcpFlagsOffset, +hdr.csumOffset wrap at
+ * 2^16); slices of readBuf are bounded by len(readBuf) here (see
+ * or_gso_split_need for the bufs side). */
 int or_gso_split(uint8_t *rb, size_t len, or_virtio_hdr hdr,
                  uint8_t *const *bufs, const size_t *buf_lens, int nbufs,
                  int *sizes, int offset, int is_v6, int *n_out) {
   int iph_len = hdr.csum_start;
   int src_off = IPV6_SRC, addr_len = 16;
   *n_out = 0;
-  /* readBuf[:iphLen] and pkt[csumStart:hdrLen] would panic otherwise */
-  if ((size_t)iph_len > len || hdr.hdr_len < hdr.csum_start) return OR_ERR_OUT_OF_RANGE;
   if (!is_v6) {
     src_off = IPV4_SRC; addr_len = 4;
-    if (len < 12) return OR_ERR_OUT_OF_RANGE;
+    if (len < 12) return OR_ERR_OUT_OF_RANGE; /* readBuf[10], readBuf[11] */
     rb[10] = 0; rb[11] = 0; /* :1388 */
   }
   int csum_at = (uint16_t)(hdr.csum_start + hdr.csum_offset); /* :1391 */
   if ((size_t)csum_at + 2 > len) return OR_ERR_OUT_OF_RANGE;
   rb[csum_at] = 0; rb[csum_at + 1] = 0; /* :1393 */
+  const int seq_at = (uint16_t)(hdr.csum_start + 4);              /* hdr.csumStart+4 (u16) */
+  const int flags_at = (uint16_t)(hdr.csum_start + TCP_FLAGS_OFF); /* :1458 (u16) */
   uint32_t first_seq = 0;
   uint8_t proto;
   if (hdr.gso_type == GSO_TCPV4 || hdr.gso_type == GSO_TCPV6) { /* :1398-1405 */
     proto = PROTO_TCP;
-    if ((size_t)hdr.csum_start + 8 > len) return OR_ERR_OUT_OF_RANGE;
-    first_seq = be32(rb + hdr.csum_start + 4);
+    if ((size_t)seq_at + 4 > len) return OR_ERR_OUT_OF_RANGE; /* Uint32(readBuf[csumStart+4:]) */
+    first_seq = be32(rb + seq_at);
   } else {
     proto = PROTO_UDP;
   }
-  if ((size_t)(src_off + 2 * addr_len) > len) return OR_ERR_OUT_OF_RANGE;
   size_t next = hdr.hdr_len;
+  if (next < len) {
+    /* the loop runs: pkt[csumStart:hdrLen] panics if csumStart > hdrLen; the
+     * pseudo-header address slices reach past len(readBuf) below 20 / 40
+     * bytes (Go would read readBuf's spare capacity: not a defined input) */
+    if (hdr.csum_start > hdr.hdr_len) return OR_ERR_OUT_OF_RANGE;
+    if ((size_t)(src_off + 2 * addr_len) > len) return OR_ERR_OUT_OF_RANGE;
+  }
   int i = 0;
   while (next < len) { /* :1408 */
     if (i == nbufs) { *n_out = i - 1; return OR_ERR_TOO_MANY_SEGMENTS; } /* :1409-1410 */
@@ -179,12 +192,15 @@ int or_gso_split(uint8_t *rb, size_t len, or_virtio_hdr hdr,
     size_t seg_len = seg_end - next;
     size_t pkt_len = hdr.hdr_len + seg_len;
     sizes[i] = (int)pkt_len;
-    if (buf_lens[i] < (size_t)offset + pkt_len) { *n_out = i; return OR_ERR_OUT_OF_RANGE; }
+    if (buf_lens[i] < (size_t)offset + or_gso_split_need(hdr, is_v6, pkt_len, seg_end == len)) {
+      *n_out = i; /* a slice of bufs[i][offset:] would panic */
+      return OR_ERR_OUT_OF_RANGE;
+    }
     uint8_t *pkt = bufs[i] + offset;
     memcpy(pkt, rb, (size_t)iph_len); /* :1419 */
     if (!is_v6) {
       if (i > 0) { /* :1426-1431 -- quirk: id0 + 1 for every i >= 1 */
-        uint16_t id = be16(pkt + 4);
+        uint16_t id = be16(pkt + 4); /* bytes past iphLen: whatever bufs[i] held */
         id += 1;
         put_be16(pkt + 4, id);
       }
@@ -197,10 +213,10 @@ int or_gso_split(uint8_t *rb, size_t len, or_virtio_hdr hdr,
            (size_t)(hdr.hdr_len - hdr.csum_start));                   /* :1442 */
     if (proto == PROTO_TCP) {
       uint32_t seq = first_seq + (uint32_t)(uint16_t)(hdr.gso_size * (uint16_t)i); /* :1445 */
-      put_be32(pkt + hdr.csum_start + 4, seq);
-      if (seg_end != len) pkt[hdr.csum_start + TCP_FLAGS_OFF] &= (uint8_t)~(TCP_FIN | TCP_PSH);
+      put_be32(pkt + seq_at, seq);
+      if (seg_end != len) pkt[flags_at] &= (uint8_t)~(TCP_FIN | TCP_PSH);
     } else {
-      put_be16(pkt + hdr.csum_start + 4,
+      put_be16(pkt + seq_at,
                (uint16_t)((uint16_t)seg_len + (uint16_t)(hdr.hdr_len - hdr.csum_start))); /* :1462-1465 */
     }
     memcpy(pkt + hdr.hdr_len, rb + next, seg_len);                   /* :1468 */
@@ -209,12 +225,32 @@ int or_gso_split(uint8_t *rb, size_t len, or_virtio_hdr hdr,
     uint64_t ph = or_pseudo_header_nofold(rb + src_off, rb + src_off + addr_len,
                                           (size_t)addr_len, proto, t_len);
     uint16_t c = (uint16_t)~or_checksum(pkt + hdr.csum_start, pkt_len - hdr.csum_start, ph);
-    put_be16(pkt + hdr.csum_start + hdr.csum_offset, c);              /* :1485-1488 */
+    put_be16(pkt + csum_at, c);                                       /* :1485-1488 */
     next += hdr.gso_size;
     i++;
   }
   *n_out = i;
   return OR_OK;
+}
+
+/* Bytes of bufs[i][offset:] one gsoSplit segment touches (gro.go:1419-1488):
+ * the packet itself plus fixed-position header writes that may lie past it
+ * (IPv4 [2:12), IPv6 [4:6), seq / UDP length at csumStart+4, the flags byte,
+ * the checksum field, all u16 positions).  A shorter buffer panics in Go. */
+size_t or_gso_split_need(or_virtio_hdr hdr, int is_v6, size_t pkt_len, int last) {
+  const int tcp = hdr.gso_type == GSO_TCPV4 || hdr.gso_type == GSO_TCPV6;
+  size_t need = pkt_len;
+  size_t t = is_v6 ? 6 : 12;
+  if (t > need) need = t;
+  t = (size_t)(uint16_t)(hdr.csum_start + 4) + (tcp ? 4 : 2);
+  if (t > need) need = t;
+  if (tcp && !last) {
+    t = (size_t)(uint16_t)(hdr.csum_start + TCP_FLAGS_OFF) + 1;
+    if (t > need) need = t;
+  }
+  t = (size_t)(uint16_t)(hdr.csum_start + hdr.csum_offset) + 2;
+  if (t > need) need = t;
+  return need;
 }
 
 /* tun/tun.go:514-632 */
@@ -694,35 +730,36 @@ out:
 /* ====================================================================== */
 static void one_pkt(int mode, uint8_t *arena, const or_pkt *p, const uint64_t *initial,
                     uint32_t i, void *out, int inplace) {
-  uint8_t *pkt = arena + p->off;
+  uint8_t *pkt = arena + ((uint64_t)p->off_lo | ((uint64_t)p->off_hi << 32));
   size_t len = p->len;
   int v6 = p->flags & 1;
-  uint8_t proto = (p->flags & 2) ? PROTO_UDP : PROTO_TCP;
+  uint8_t proto = p->proto;
   size_t aoff = v6 ? IPV6_SRC : IPV4_SRC, alen = v6 ? 16 : 4;
   uint16_t cs = p->csum_start, co = p->csum_offset;
+  uint16_t at = (uint16_t)(cs + co); /* u16 field position, gro.go:1391 / :1503 */
   switch (mode) {
     case 0: /* FOLD: checksum(b, initial) */
       ((uint16_t *)out)[i] = or_checksum(pkt, len, initial ? initial[i] : 0);
       break;
     case 1: { /* L4_FILL: gro.go:1469-1488 with the field treated as zero */
-      uint8_t save0 = pkt[cs + co], save1 = pkt[cs + co + 1];
-      pkt[cs + co] = 0; pkt[cs + co + 1] = 0;
+      uint8_t save0 = pkt[at], save1 = pkt[at + 1];
+      pkt[at] = 0; pkt[at + 1] = 0;
       uint64_t ph = or_pseudo_header_nofold(pkt + aoff, pkt + aoff + alen, alen, proto,
                                             (uint16_t)(len - cs));
       uint16_t c = (uint16_t)~or_checksum(pkt + cs, len - cs, ph);
       ((uint16_t *)out)[i] = c;
-      if (inplace) put_be16(pkt + cs + co, c);
-      else { pkt[cs + co] = save0; pkt[cs + co + 1] = save1; }
+      if (inplace) put_be16(pkt + at, c);
+      else { pkt[at] = save0; pkt[at + 1] = save1; }
       break;
     }
     case 2: /* VALIDATE: checksumValid */
-      ((uint8_t *)out)[i] = (uint8_t)or_checksum_valid(pkt, len, (uint8_t)cs, proto, v6);
+      ((uint8_t *)out)[i] = (uint8_t)checksum_valid_at(pkt, len, cs, proto, v6); /* u16 iphLen */
       break;
     case 3: { /* PARTIAL: gsoNoneChecksum */
-      uint8_t save0 = pkt[(uint16_t)(cs + co)], save1 = pkt[(uint16_t)(cs + co) + 1];
+      uint8_t save0 = pkt[at], save1 = pkt[at + 1];
       or_gso_none_checksum(pkt, len, cs, co);
-      ((uint16_t *)out)[i] = be16(pkt + (uint16_t)(cs + co));
-      if (!inplace) { pkt[(uint16_t)(cs + co)] = save0; pkt[(uint16_t)(cs + co) + 1] = save1; }
+      ((uint16_t *)out)[i] = be16(pkt + at);
+      if (!inplace) { pkt[at] = save0; pkt[at + 1] = save1; }
       break;
     }
     case 4: { /* IP4HDR: gro.go:1134-1138 */

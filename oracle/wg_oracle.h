@@ -77,6 +77,8 @@ int or_gso_none_checksum(uint8_t *read_buf, size_t len, uint16_t csum_start,
 int or_gso_split(uint8_t *read_buf, size_t len, or_virtio_hdr hdr,
                  uint8_t *const *bufs, const size_t *buf_lens, int nbufs,
                  int *sizes, int offset, int is_v6, int *n_out);
+/* bytes of bufs[i][offset:] a gsoSplit segment of pkt_len bytes writes */
+size_t or_gso_split_need(or_virtio_hdr hdr, int is_v6, size_t pkt_len, int last);
 /* tun/tun.go:514-632.  read_buf starts with the 10-byte virtio header. */
 int or_handle_virtio_read(uint8_t *read_buf, size_t n, uint8_t *const *bufs,
                           const size_t *buf_lens, int nbufs, int *sizes,
@@ -90,12 +92,14 @@ int or_handle_gro(uint8_t **bufs, size_t *lens, size_t *caps, int n,
                   int *n_to_write);
 
 /* Batch helpers used by tests and by bench.py's cpu_baseline leg. */
-typedef struct or_pkt {
-  uint64_t off;
+typedef struct or_pkt { /* same layout as wgcs_pkt (include/wgcsum.h) */
+  uint32_t off_lo;
+  uint16_t off_hi;
+  uint8_t proto;
+  uint8_t flags; /* bit0 IPv6 */
   uint32_t len;
   uint16_t csum_start;
-  uint8_t csum_offset;
-  uint8_t flags; /* bit0 IPv6, bit1 UDP */
+  uint16_t csum_offset;
 } or_pkt;
 /* mode values match include/wgcsum.h WGCS_MODE_* */
 void or_checksum_batch(int mode, uint8_t *arena, const or_pkt *pkts,

@@ -44,6 +44,13 @@ def fold_vectors(rng):
     return out
 
 
+def rows(p):
+    """wgcs_pkt rows as [off, len, csum_start, csum_offset, proto, flags]."""
+    off = synth.pkt_off(p)
+    return [[int(off[i]), int(x["len"]), int(x["csum_start"]), int(x["csum_offset"]), int(x["proto"]), int(x["flags"])]
+            for i, x in enumerate(p)]
+
+
 def frame_vectors():
     arena, pkts, kinds = synth.make_batch(48, 1501, kinds="mixed", seed=SEED, stride=1505)
     bad, _, _ = synth.make_batch(16, 1501, kinds="mixed", seed=SEED + 1, stride=1505, valid=False)
@@ -51,17 +58,17 @@ def frame_vectors():
     p2 = np.zeros(64, pkts.dtype)
     p2[:48] = pkts
     _, pb, _ = synth.make_batch(16, 1501, kinds="mixed", seed=SEED + 1, stride=1505, valid=False)
-    pb["off"] += 48 * 1505
+    synth.set_pkt_off(pb, synth.pkt_off(pb) + np.uint64(48 * 1505))
     p2[48:] = pb
     rec = {
         "arena_hex": arena.tobytes().hex(),
-        "pkts": [[int(x["off"]), int(x["len"]), int(x["csum_start"]), int(x["csum_offset"]), int(x["flags"])] for x in p2],
+        "pkts": rows(p2),
     }
     for name, mode in (("validate", 2), ("fill", 1), ("partial", 3), ("fold", 0)):
         rec[name] = [int(v) for v in oracle.checksum_batch(mode, arena.copy(), p2)]
     p4 = p2.copy()
     p4 = p4[(p4["flags"] & 1) == 0]
-    rec["ip4hdr_pkts"] = [[int(x["off"]), int(x["len"]), int(x["csum_start"]), int(x["csum_offset"]), int(x["flags"])] for x in p4]
+    rec["ip4hdr_pkts"] = rows(p4)
     rec["ip4hdr"] = [int(v) for v in oracle.checksum_batch(4, arena.copy(), p4)]
     return rec
 

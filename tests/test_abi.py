@@ -43,9 +43,12 @@ def test_header_is_c_and_layouts(tmp_path):
     src.write_text(
         '#include "wgcsum.h"\n#include <stddef.h>\n'
         "_Static_assert(sizeof(wgcs_pkt) == 16, \"pkt\");\n"
+        "_Static_assert(offsetof(wgcs_pkt, off_hi) == 4, \"off_hi\");\n"
+        "_Static_assert(offsetof(wgcs_pkt, proto) == 6, \"proto\");\n"
+        "_Static_assert(offsetof(wgcs_pkt, flags) == 7, \"flags\");\n"
         "_Static_assert(offsetof(wgcs_pkt, len) == 8, \"len\");\n"
         "_Static_assert(offsetof(wgcs_pkt, csum_start) == 12, \"cs\");\n"
-        "_Static_assert(offsetof(wgcs_pkt, flags) == 15, \"flags\");\n"
+        "_Static_assert(offsetof(wgcs_pkt, csum_offset) == 14, \"co\");\n"
         "_Static_assert(sizeof(wgcs_gso_job) == 16, \"job\");\n"
         "_Static_assert(sizeof(wgcs_virtio_hdr) == 10, \"virtio_net_hdr is 10 bytes (gro.go:69-71)\");\n"
         "int main(void) { return 0; }\n")
@@ -60,14 +63,38 @@ def test_python_constants_match_header():
         if hasattr(_lib, short):
             assert getattr(_lib, short) == val, name
     assert tun.PKT_DTYPE.itemsize == 16 and tun.GSO_JOB_DTYPE.itemsize == 16
+    for f in ("off_lo", "off_hi", "proto", "flags", "len", "csum_start", "csum_offset"):
+        assert tun.PKT_DTYPE.fields[f][1] == oracle_dtype().fields[f][1], f
     assert C.sizeof(_lib.VirtioHdr) == 10
     assert d["WGCS_MODE_VALIDATE"] == _lib.MODE_VALIDATE
+
+
+def oracle_dtype():
+    import oracle
+    return oracle.PKT_DTYPE
+
+
+def test_pkt_set_matches_python_layout(tmp_path):
+    """wgcs_pkt_set (header-only helper) packs what tun.set_pkt_off + fields do."""
+    src = tmp_path / "p.c"
+    src.write_text('#include "wgcsum.h"\n#include <stdio.h>\n#include <string.h>\n'
+                   "int main(void) { wgcs_pkt p; unsigned char b[16]; "
+                   "wgcs_pkt_set(&p, 0x123456789ABCull, 1500, 20, 40000, 17, WGCS_PKT_V6); "
+                   "memcpy(b, &p, 16); for (int i = 0; i < 16; i++) printf(\"%02x\", b[i]); return 0; }\n")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.dirname(HDR), str(src), "-o",
+                    str(tmp_path / "p")], check=True)
+    out = subprocess.run([str(tmp_path / "p")], capture_output=True, text=True, check=True).stdout
+    p = np.zeros(1, tun.PKT_DTYPE)
+    tun.set_pkt_off(p, [0x123456789ABC])
+    p["len"], p["csum_start"], p["csum_offset"], p["proto"], p["flags"] = 1500, 20, 40000, 17, tun.PKT_V6
+    assert out == p.tobytes().hex()
+    assert int(tun.pkt_off(p)[0]) == 0x123456789ABC
 
 
 def test_version_and_errors():
     L = wireguard_amd.load()
     assert L.wgcs_abi_version() == _defines()["WGCS_ABI_VERSION"]
-    for code in [0, -1, -2, -3, -4, -5, -6, -7, -8, -9, -10, -11, -12, -13, -14, -15, -100, -101, -102]:
+    for code in [0, -1, -2, -3, -4, -5, -6, -7, -8, -9, -10, -11, -12, -13, -14, -15, -16, -17, -100, -101, -102]:
         assert L.wgcs_strerror(code) and L.wgcs_strerror(code) != b"unknown status"
     assert L.wgcs_strerror(-9999) == b"unknown status"
 
@@ -99,5 +126,6 @@ def test_synth_descriptors_layout():
     from wireguard_amd import synth
     arena, pkts, k = synth.make_batch(64, 1500, kinds="mixed")
     assert pkts.dtype == tun.PKT_DTYPE
-    assert (pkts["off"] == np.arange(64) * 1500).all()
+    assert (tun.pkt_off(pkts) == np.arange(64) * 1500).all()
     assert set(np.unique(pkts["csum_offset"])) <= {6, 16}
+    assert ((pkts["proto"] == 17) == (pkts["csum_offset"] == 6)).all()

@@ -5,21 +5,22 @@ import pytest
 
 import oracle
 from wireguard_amd import synth
-from wireguard_amd.tun import (MODE_FOLD, MODE_IP4HDR, MODE_L4_FILL, MODE_PARTIAL, MODE_VALIDATE, PKT_DTYPE, PKT_UDP,
-                               PKT_V6)
+from wireguard_amd.tun import (MODE_FOLD, MODE_IP4HDR, MODE_L4_FILL, MODE_PARTIAL, MODE_VALIDATE, PKT_DTYPE, PKT_V6,
+                               pkt_off, set_pkt_off)
 
 pytestmark = pytest.mark.gpu
 
 INITS = [0, 0xFFFF, 2**64 - 1, 1, 0x1234567890ABCDEF, 0xFFFF0000FFFF0000]
 
 
-def _pkts(offs, lens, cs=0, co=0, flags=0):
+def _pkts(offs, lens, cs=0, co=0, flags=0, proto=6):
     p = np.zeros(len(offs), dtype=PKT_DTYPE)
-    p["off"] = offs
+    set_pkt_off(p, offs)
     p["len"] = lens
     p["csum_start"] = cs
     p["csum_offset"] = co
     p["flags"] = flags
+    p["proto"] = proto
     return p
 
 
@@ -91,18 +92,20 @@ def test_validate_random_descriptors(dev):
     rng = np.random.default_rng(5)
     arena = rng.integers(0, 256, size=1 << 20, dtype=np.uint8)
     n = 4000
-    flags = rng.integers(0, 4, size=n)
+    flags = rng.integers(0, 2, size=n)
+    proto = rng.integers(0, 256, size=n)  # checksumValid takes any protocol byte
+    proto[::2] = np.where(rng.integers(0, 2, size=len(proto[::2])) == 1, 17, 6)
     lens = rng.integers(40, 3000, size=n)
     cs = np.minimum(rng.integers(0, 80, size=n), lens - 20)
     cs[::3] = np.where(flags[::3] & 1, 40, 20)
     offs = np.arange(n) * 3003 + rng.integers(0, 3, size=n)  # disjoint packets, odd alignments
     arena = rng.integers(0, 256, size=n * 3003 + 64, dtype=np.uint8)
-    p = _pkts(offs, lens, cs, 0, flags)
+    p = _pkts(offs, lens, cs, 0, flags, proto)
     got, want, _, _ = _both(dev, MODE_VALIDATE, arena, p)
     assert np.array_equal(got, want)
-    co = np.where(flags & PKT_UDP, 6, 16)
+    co = np.where(proto == 17, 6, 16)
     ok = cs + co + 2 <= lens
-    p = _pkts(offs[ok], lens[ok], cs[ok], co[ok], flags[ok])
+    p = _pkts(offs[ok], lens[ok], cs[ok], co[ok], flags[ok], proto[ok])
     got, want, _, _ = _both(dev, MODE_L4_FILL, arena, p)
     assert np.array_equal(got, want)
     # force a valid checksum into every packet and validate
@@ -128,6 +131,37 @@ def test_partial_gso_none(dev):
     assert np.array_equal(got, want) and np.array_equal(ag, ac)
     got, want, _, _ = _both(dev, MODE_PARTIAL, arena, p)
     assert np.array_equal(got, want)
+
+
+def test_partial_u16_offsets(dev):
+    """gsoNoneChecksum's csumStart + csumOffset is a uint16 sum (gro.go:1503):
+    offsets across 0..65535, including wrapped positions before csumStart."""
+    rng = np.random.default_rng(13)
+    n = 400
+    lens = rng.integers(64, 65536, size=n)
+    cs = rng.integers(0, 65536, size=n) % lens
+    at = rng.integers(0, 2**16, size=n) % (lens - 1)  # field position inside the packet
+    co = (at - cs) % 65536                             # any u16 offset, wrapping when at < cs
+    co[:4] = [65535, 256, 4096, 40000]
+    at[:4] = (cs[:4] + co[:4]) % 65536
+    ok = at + 2 <= lens
+    lens, cs, co = lens[ok], cs[ok], co[ok]
+    m = len(lens)
+    stride = 65539
+    arena = rng.integers(0, 256, size=m * stride + 64, dtype=np.uint8)
+    p = _pkts(np.arange(m) * stride + rng.integers(0, 3, size=m), lens, cs, co)
+    assert (p["csum_offset"] > 255).sum() > m // 2
+    got, want, ag, ac = _both(dev, MODE_PARTIAL, arena, p, inplace=True)
+    assert np.array_equal(got, want) and np.array_equal(ag, ac)
+    got, want, _, _ = _both(dev, MODE_L4_FILL, arena, p)
+    assert np.array_equal(got, want)
+    # the single-call drop-in with the same u16 offsets
+    for i in range(8):
+        pk = bytearray(arena[int(pkt_off(p)[i]): int(pkt_off(p)[i]) + int(lens[i])].tobytes())
+        pk2 = bytearray(pk)
+        assert dev.gso_none_checksum(pk, int(cs[i]), int(co[i])) is None
+        oracle.lib().or_gso_none_checksum(np.frombuffer(pk2, np.uint8).ctypes.data, len(pk2), int(cs[i]), int(co[i]))
+        assert pk == pk2
 
 
 def test_partial_all_zero_is_zero_not_ffff(dev):
@@ -161,58 +195,23 @@ def test_reference_shaped_single_calls(dev):
         for ini in INITS:
             assert dev.checksum(b, ini) == oracle.checksum(b, ini)
     arena, pkts, kinds = synth.make_batch(8, 1500, kinds="mixed")
+    offs = pkt_off(pkts)
     for i in range(8):
-        pkt = arena[pkts["off"][i]: pkts["off"][i] + 1500].tobytes()
+        pkt = arena[offs[i]: offs[i] + 1500].tobytes()
         v6 = bool(pkts["flags"][i] & PKT_V6)
-        proto = 17 if pkts["flags"][i] & PKT_UDP else 6
+        proto = int(pkts["proto"][i])
         assert dev.checksum_valid(pkt, 40 if v6 else 20, proto, v6)
         bad = bytearray(pkt)
         bad[-1] ^= 1
         assert not dev.checksum_valid(bytes(bad), 40 if v6 else 20, proto, v6)
+    # any protocol byte and any iphLen (checksumValid's uint8 arguments)
+    for proto in (0, 1, 6, 17, 41, 58, 132, 255):
+        for iph in (0, 19, 20, 21, 40, 255):
+            b = rng.integers(0, 256, size=300, dtype=np.uint8).tobytes()
+            for v6 in (False, True):
+                assert dev.checksum_valid(b, iph, proto, v6) == oracle.checksum_valid(b, iph, proto, v6)
     rb = bytearray(rng.integers(0, 256, size=777, dtype=np.uint8).tobytes())
     rb2 = bytearray(rb)
     assert dev.gso_none_checksum(rb, 21, 16) is None
     oracle.lib().or_gso_none_checksum((np.frombuffer(rb2, np.uint8)).ctypes.data, len(rb2), 21, 16)
     assert rb == rb2
-
-
-@pytest.fixture(scope="module")
-def flat_dev():
-    """A context launched with the opt-in flat-group mapping (16-lane rows,
-    4 back-to-back frames streamed as one run)."""
-    import os
-
-    from wireguard_amd.tun import Device
-
-    keys = ("WGCS_LANES_PER_PKT", "WGCS_FLAT", "WGCS_UNROLL")
-    old = {k: os.environ.get(k) for k in keys}
-    os.environ.update({"WGCS_LANES_PER_PKT": "16", "WGCS_FLAT": "1", "WGCS_UNROLL": "4"})
-    try:
-        d = Device(0)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    yield d
-    d.close()
-
-
-@pytest.mark.parametrize("kinds", ["tcp4", "udp4", "tcp6", "mixed"])
-@pytest.mark.parametrize("frame_len,stride", [(1500, None), (1501, None), (1499, None), (9000, None), (300, None),
-                                              (1500, 1504), (61, None)])
-@pytest.mark.parametrize("valid", [True, False])
-def test_flat_group_path(flat_dev, kinds, frame_len, stride, valid):
-    """Back-to-back groups take the flat stream (clean chunks branch-free,
-    dirty chunks settled once per group); gaps (stride), IPv6-in-mixed groups
-    and short frames exercise its fallback to the row path."""
-    arena, pkts, _ = synth.make_batch(1027, frame_len, kinds=kinds, stride=stride, valid=valid,
-                                      seed=frame_len + len(kinds))
-    got, want, _, _ = _both(flat_dev, MODE_VALIDATE, arena, pkts)
-    assert np.array_equal(got, want)
-    assert bool(got.all()) == valid
-    got, want, _, _ = _both(flat_dev, MODE_L4_FILL, arena, pkts)
-    assert np.array_equal(got, want)
-    got, want, ag, ac = _both(flat_dev, MODE_L4_FILL, arena, pkts, inplace=True)
-    assert np.array_equal(got, want) and np.array_equal(ag, ac)

@@ -15,7 +15,7 @@ import pytest
 
 import oracle
 from wireguard_amd import shard, synth
-from wireguard_amd.tun import GSO_JOB_DTYPE, MODE_L4_FILL, MODE_VALIDATE, PKT_DTYPE
+from wireguard_amd.tun import GSO_JOB_DTYPE, MODE_L4_FILL, MODE_VALIDATE, PKT_DTYPE, pkt_off, set_pkt_off
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -27,7 +27,7 @@ def S():
 
 
 def _field_pos(pkts):
-    return pkts["off"].astype(np.int64) + pkts["csum_start"].astype(np.int64) + pkts["csum_offset"].astype(np.int64)
+    return pkt_off(pkts).astype(np.int64) + pkts["csum_start"].astype(np.int64) + pkts["csum_offset"].astype(np.int64)
 
 
 @pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg5"])
@@ -58,7 +58,7 @@ def test_checksum_batch_properties(dev, cfg):
 
     # corrupt 97 frames on the device: VALIDATE rejects exactly those
     bad = np.sort(rng.choice(n, size=97, replace=False))
-    pos = pkts_np["off"][bad].astype(np.int64) + rng.integers(0, flen, size=97)
+    pos = pkt_off(pkts_np)[bad].astype(np.int64) + rng.integers(0, flen, size=97)
     idx = torch.from_numpy(pos).cuda()
     arena[idx] ^= torch.tensor(0x5A, dtype=torch.uint8, device="cuda")
     dev.checksum_batch(MODE_VALIDATE, arena, pkts, n, out, stream=S())
@@ -100,10 +100,11 @@ def test_gso_cfg4_properties(dev):
     # every produced segment validates (checksum kernel over the split kernel's output)
     slots = [(j, i) for j in range(n_jobs) for i in range(45)]
     segs = np.zeros(len(slots), PKT_DTYPE)
-    segs["off"] = [(j * max_segs + i) * stride + offset for j, i in slots]
+    set_pkt_off(segs, [(j * max_segs + i) * stride + offset for j, i in slots])
     segs["len"] = [sizes[j, i] for j, i in slots]
     segs["csum_start"] = 20
     segs["csum_offset"] = 16
+    segs["proto"] = 6
     d_segs = torch.from_numpy(segs.view(np.uint8)).cuda()
     valid = torch.zeros(len(slots), dtype=torch.uint8, device="cuda")
     dev.checksum_batch(MODE_VALIDATE, d_out, d_segs, len(slots), valid, stream=S())

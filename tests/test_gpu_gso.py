@@ -7,8 +7,8 @@ import pytest
 import oracle
 from wireguard_amd import synth
 from wireguard_amd._lib import (ERR_BAD_IP_VERSION, ERR_CSUM_OFFSET, ERR_HDR_LEN, ERR_IP_GSO_MISMATCH,
-                                ERR_PACKET_TOO_SHORT, ERR_READ_OVERFLOW, ERR_SHORT_BUFFER, ERR_TCP_HDR_LEN,
-                                ERR_TOO_MANY_SEGMENTS, ERR_UNSUPPORTED_GSO, VirtioHdr)
+                                ERR_OUT_OF_RANGE, ERR_PACKET_TOO_SHORT, ERR_READ_OVERFLOW, ERR_SHORT_BUFFER,
+                                ERR_TCP_HDR_LEN, ERR_TOO_MANY_SEGMENTS, ERR_UNSUPPORTED_GSO, VirtioHdr)
 from wireguard_amd.tun import GSO_JOB_DTYPE
 
 pytestmark = pytest.mark.gpu
@@ -16,25 +16,41 @@ pytestmark = pytest.mark.gpu
 SENT = 0xA5
 
 
-def _bufs(nbufs, size):
-    return [np.full(size, SENT, dtype=np.uint8) for _ in range(nbufs)]
+def _bufs(nbufs, size, fill=SENT):
+    return [np.full(size, fill, dtype=np.uint8) for _ in range(nbufs)]
 
 
 def _code(err):
     return 0 if err is None else err.code
 
 
-def run_both(dev, vpkt: bytes, nbufs=128, bufsize=65535, offset=16):
+def run_both(dev, vpkt: bytes, nbufs=128, bufsize=65535, offset=16, fill=SENT):
     rb_o = np.frombuffer(bytearray(vpkt), dtype=np.uint8).copy()
     rb_p = rb_o.copy()
-    bo, bp = _bufs(nbufs, bufsize), _bufs(nbufs, bufsize)
+    bo, bp = _bufs(nbufs, bufsize, fill), _bufs(nbufs, bufsize, fill)
     rc_o, n_o, sz_o = oracle.handle_virtio_read(rb_o, bo, offset)
     sz_p = [0] * nbufs
     n_p, err = dev.handle_virtio_read(rb_p, bp, sz_p, offset)
     return (rc_o, n_o, sz_o, bo, rb_o), (_code(err), n_p, sz_p, bp, rb_p)
 
 
-def assert_same(o, p, check_bufs=True):
+def run_both_raw(dev, rb: bytes, hdr: tuple, is_v6: bool, nbufs=16, bufsize=9000, offset=16, fill=SENT):
+    """gsoSplit(readBuf, hdr, ...) with the caller's header (gro.go:1373)."""
+    rb_o = np.frombuffer(bytearray(rb), dtype=np.uint8).copy()
+    rb_p = rb_o.copy()
+    bo, bp = _bufs(nbufs, bufsize, fill), _bufs(nbufs, bufsize, fill)
+    rc_o, n_o, sz_o = oracle.gso_split(rb_o, hdr, bo, offset, is_v6)
+    sz_p = [0] * nbufs
+    n_p, err = dev.gso_split(rb_p, VirtioHdr(*hdr), bp, sz_p, offset, is_v6)
+    return (rc_o, n_o, sz_o, bo, rb_o), (_code(err), n_p, sz_p, bp, rb_p)
+
+
+def assert_same(o, p, check_bufs=True, offset=16, fill=SENT):
+    """check_bufs: True -- every byte of every buffer; "packets" -- the
+    packets bufs[i][offset:offset+sizes[i]], and the product leaves every
+    other byte alone (gsoSplit's header writes that land past a packet's end,
+    e.g. a checksum field beyond pktLen, are not part of the result:
+    DESIGN.md §8)."""
     rc_o, n_o, sz_o, bo, rb_o = o
     rc_p, n_p, sz_p, bp, rb_p = p
     assert rc_p == rc_o, (rc_p, rc_o)
@@ -43,7 +59,12 @@ def assert_same(o, p, check_bufs=True):
     if rc_o in (0, ERR_TOO_MANY_SEGMENTS):
         assert sz_p[:written] == sz_o[:written]
         assert np.array_equal(rb_p, rb_o), "readBuf mutation differs"
-        if check_bufs:
+        if check_bufs == "packets":
+            for i in range(len(bo)):
+                k = sz_o[i] if i < written else 0
+                assert np.array_equal(bp[i][offset: offset + k], bo[i][offset: offset + k]), f"segment {i} differs"
+                assert (bp[i][:offset] == fill).all() and (bp[i][offset + k:] == fill).all(), f"bytes past segment {i}"
+        elif check_bufs:
             for i in range(len(bo)):
                 assert np.array_equal(bp[i], bo[i]), f"segment {i} differs"
 
@@ -98,26 +119,36 @@ def test_ipv4_options_and_tcp_options(dev):
 
 
 def test_gso_none_paths(dev):
+    """GSO_NONE (+ NEEDS_CSUM: gsoNoneChecksum with a uint16 csumStart +
+    csumOffset anywhere in the packet, gro.go:1497-1517)."""
     rng = np.random.default_rng(4)
-    for trial in range(40):
-        plen = int(rng.integers(1, 3000))
+    big_offsets = 0
+    for trial in range(120):
+        plen = int(rng.integers(1, 3000)) if trial % 3 else int(rng.integers(3000, 65536))
         pkt = rng.integers(0, 256, size=plen, dtype=np.uint8)
         pkt[0] = 0x45
-        cs = int(rng.integers(0, max(1, plen - 2)))
-        co = int(rng.integers(0, max(1, min(60, plen - cs - 1))))
+        cs = int(rng.integers(0, plen))
+        if plen >= 2 and rng.random() < 0.8:
+            at = int(rng.integers(0, plen - 1))  # field inside the packet, any u16 offset (wraps when at < cs)
+            co = (at - cs) % 65536
+        else:
+            co = int(rng.integers(0, 65536))
+        big_offsets += co > 255
         flags = int(rng.integers(0, 2))
         hdr = np.zeros(10, np.uint8)
         hdr[0] = flags
         hdr[6:8] = np.frombuffer(np.uint16(cs).tobytes(), np.uint8)
         hdr[8:10] = np.frombuffer(np.uint16(co).tobytes(), np.uint8)
         vp = hdr.tobytes() + pkt.tobytes()
-        bufsize = int(rng.choice([65535, plen + 16, plen + 15, 100]))
+        bufsize = int(rng.choice([65535 + 16, plen + 16, plen + 15, 100]))
         o, p = run_both(dev, vp, nbufs=4, bufsize=bufsize, offset=16)
-        if flags and cs + co + 2 > plen:
-            continue  # the reference panics on this input; not comparable
+        if o[0] == ERR_OUT_OF_RANGE:
+            assert p[0] == ERR_OUT_OF_RANGE  # the reference panics on this input
+            continue
         assert_same(o, p)
         if bufsize < plen + 16:
             assert o[0] == ERR_READ_OVERFLOW
+    assert big_offsets > 50
 
 
 def test_validation_errors(dev):
@@ -155,21 +186,108 @@ def test_validation_errors(dev):
             assert_same(o, p)
 
 
-def test_fuzz_headers(dev):
-    rng = np.random.default_rng(17)
-    base = bytearray(synth.make_super_packet(8000, 1000))
-    for _ in range(150):
-        b = bytearray(base)
-        k = int(rng.integers(1, 4))
-        for _ in range(k):
-            pos = int(rng.choice([1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 10 + 20 + 12]))
-            b[pos] = int(rng.integers(0, 256))
-        if rng.random() < 0.3:
-            b = b[: int(rng.integers(10, len(b)))]
-        o, p = run_both(dev, bytes(b), nbufs=16, bufsize=9000)
-        if p[0] == -13 and o[0] in (0, ERR_TOO_MANY_SEGMENTS, -13):
-            continue  # product-documented limits or reference panic
-        assert_same(o, p)
+def _fuzz_header(rng, base: bytearray, raw: bool):
+    """Mutate the virtio header / IP version / TCP data offset of a valid
+    super-packet: any header geometry handleVirtioRead or gsoSplit accepts,
+    including IP headers shorter than 20 / 40 bytes, headers over 240 bytes,
+    checksum fields outside the header, wrapped uint16 positions."""
+    b = bytearray(base)
+    plen = len(b) - 10
+    f = lambda a, v: b.__setitem__(slice(a, a + 2), int(v % 65536).to_bytes(2, "little"))  # noqa: E731
+    if rng.random() < 0.2:
+        b[0] = int(rng.integers(0, 256))
+    if rng.random() < 0.3:
+        b[1] = int(rng.choice([0, 1, 4, 5, int(rng.integers(0, 256))]))
+    cs = int(rng.choice([int.from_bytes(b[6:8], "little"), int(rng.integers(0, 64)), int(rng.integers(0, 400)),
+                         int(rng.integers(65500, 65536))], p=[0.25, 0.35, 0.35, 0.05]))
+    f(6, cs)
+    if rng.random() < 0.8 and plen >= 2:
+        at = int(rng.integers(0, min(plen - 1, 600))) if rng.random() < 0.7 else int(rng.integers(0, plen - 1))
+        f(8, at - cs)
+    else:
+        f(8, int(rng.integers(0, 65536)))
+    if rng.random() < 0.5:
+        f(2, int(rng.choice([cs + 8, cs + 20, int(rng.integers(0, 600)), int(rng.integers(0, 65536))])))
+    if rng.random() < 0.4:
+        f(4, int(rng.choice([0, 1, 7, int(rng.integers(1, 3000)), 65535])))
+    if rng.random() < 0.3:
+        b[10] = (int(rng.choice([4, 6, int(rng.integers(0, 16))])) << 4) | (b[10] & 0xF)
+    if 10 + cs + 12 < len(b) and rng.random() < 0.5:
+        b[10 + cs + 12] = int(rng.choice([0x50, 0x80, 0xF0, int(rng.integers(0, 256))]))
+    if rng.random() < 0.25:
+        b = b[: int(rng.integers(10, len(b) + 1))]
+    return bytes(b)
+
+
+@pytest.mark.parametrize("raw", [False, True])
+def test_fuzz_headers(dev, raw):
+    """>= 1000 mutated headers per entry point.  The only cases not compared
+    byte for byte are those where the ORACLE reports a reference panic
+    (OUT_OF_RANGE); the product must report the same there."""
+    rng = np.random.default_rng(17 + raw)
+    bases = [bytearray(synth.make_super_packet(t, g, seed=t, v6=v6, udp=u))
+             for t, g, v6, u in [(8000, 1000, False, False), (3000, 500, True, False), (6000, 1448, False, True),
+                                 (2500, 700, True, True), (1200, 100, False, False), (20000, 1460, False, False)]]
+    compared = panics = 0
+    trials = 1500 if raw else 1100
+    for trial in range(trials):
+        vp = _fuzz_header(rng, bases[trial % len(bases)], raw)
+        nbufs = int(rng.choice([4, 16, 64]))
+        bufsize = int(rng.choice([2000, 9000, 65535]))
+        fill = int(rng.choice([SENT, 0x00, 0xFF]))
+        offset = int(rng.choice([16, 10, 3, 0]))
+        if raw:
+            h = tuple([vp[0], vp[1]] + [int.from_bytes(vp[k:k + 2], "little") for k in (2, 4, 6, 8)])
+            o, p = run_both_raw(dev, vp[10:], h, bool(rng.integers(0, 2)), nbufs, bufsize, offset, fill)
+        else:
+            o, p = run_both(dev, vp, nbufs, bufsize, offset, fill)
+        if o[0] == ERR_OUT_OF_RANGE:
+            assert p[0] == ERR_OUT_OF_RANGE, (trial, p[0])
+            panics += 1
+            continue
+        assert_same(o, p, check_bufs="packets", offset=offset, fill=fill)
+        compared += 1
+    assert compared >= 550 and compared + panics == trials
+
+
+def test_general_path_geometries(dev):
+    """Targeted header geometries the row-streaming path does not take."""
+    cases = []
+    base4 = synth.make_super_packet(6000, 1000, seed=5)
+    base6 = synth.make_super_packet(6000, 1000, seed=6, v6=True)
+    for cs in (0, 1, 4, 5, 6, 11, 12, 19):  # IPv4 header shorter than 20 bytes (cs == 5: bufs' own byte 5)
+        for co in (6, 16, 40, 65535 - cs + 3):
+            h = bytearray(base4)
+            h[6:8] = cs.to_bytes(2, "little")
+            h[8:10] = co.to_bytes(2, "little")
+            h[1] = 5  # UDP_L4: hdrLen = cs + 8
+            cases.append(bytes(h))
+    for cs in (300, 600):  # header over 240 bytes
+        h = bytearray(base6)
+        h[1] = 4
+        h[6:8] = cs.to_bytes(2, "little")
+        h[10 + cs + 12] = 0x80
+        cases.append(bytes(h))
+    for fill in (SENT, 0xFF, 0x00):
+        for vp in cases:
+            o, p = run_both(dev, vp, nbufs=16, bufsize=9000, fill=fill)
+            if o[0] == ERR_OUT_OF_RANGE:
+                assert p[0] == ERR_OUT_OF_RANGE
+                continue
+            assert_same(o, p, check_bufs="packets", fill=fill)
+
+
+def test_raw_gso_type_none_is_udp(dev):
+    """gsoSplit itself treats any non-TCP gso_type (0 included) as UDP
+    (gro.go:1398-1405): with gso_size 100 a 1000-byte packet splits into ~10
+    segments (the packed output layout must size for them)."""
+    rng = np.random.default_rng(8)
+    rb = bytearray(rng.integers(0, 256, size=1000, dtype=np.uint8).tobytes())
+    rb[0] = 0x45
+    for gtype, gso in ((0, 100), (0, 1), (0, 0), (2, 333), (5, 100)):
+        o, p = run_both_raw(dev, bytes(rb), (1, gtype, 28, gso, 20, 6), False, nbufs=32, bufsize=2000)
+        assert o[0] in (0, ERR_TOO_MANY_SEGMENTS) and o[1] >= 9
+        assert_same(o, p, check_bufs="packets")
 
 
 def test_raw_gso_split(dev):

@@ -84,10 +84,10 @@ def test_synth_frames_validate(kinds):
     assert not oracle.checksum_batch(2, bad, pkts).any()
     # single-packet entry point agrees with the batch helper
     for i in range(10):
-        o = int(pkts["off"][i])
+        o = int(synth.pkt_off(pkts)[i])
         pkt = arena[o: o + 1500].tobytes()
         v6 = bool(pkts["flags"][i] & 1)
-        proto = 17 if pkts["flags"][i] & 2 else 6
+        proto = int(pkts["proto"][i])
         assert oracle.checksum_valid(pkt, 40 if v6 else 20, proto, v6)
 
 

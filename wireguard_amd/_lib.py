@@ -39,7 +39,7 @@ ERR_NO_DEVICE = -102
 
 MODE_FOLD, MODE_L4_FILL, MODE_VALIDATE, MODE_PARTIAL, MODE_IP4HDR = 0, 1, 2, 3, 4
 F_INPLACE = 0x1
-PKT_V6, PKT_UDP = 0x01, 0x02
+PKT_V6 = 0x01
 
 
 class WgcsError(RuntimeError):
@@ -62,7 +62,8 @@ def declared_symbols() -> list[str]:
     """Function names declared in include/wgcsum.h."""
     with open(HEADER_PATH) as f:
         src = f.read()
-    return sorted(set(re.findall(r"\b(wgcs_[a-z0-9_]+)\s*\(", src)))
+    inline = set(re.findall(r"static inline [^(]*\b(wgcs_[a-z0-9_]+)\s*\(", src))  # header-only helpers
+    return sorted(set(re.findall(r"\b(wgcs_[a-z0-9_]+)\s*\(", src)) - inline)
 
 
 def load() -> C.CDLL:

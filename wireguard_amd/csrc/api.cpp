@@ -103,8 +103,6 @@ int wgcs_init(int device, wgcs_ctx** out) {
   if (lpp && (atoi(lpp) == 64 || atoi(lpp) == 32)) ctx->tune.lanes_per_pkt = atoi(lpp);
   const char* nt = getenv("WGCS_NT");
   if (nt) ctx->tune.nt = atoi(nt) ? 1 : 0;
-  const char* fl = getenv("WGCS_FLAT");
-  if (fl) ctx->tune.flat = atoi(fl) ? 1 : 0;
   const char* al = getenv("WGCS_ALIGN");
   if (al && (atoi(al) == 16 || atoi(al) == 32 || atoi(al) == 64 || atoi(al) == 128)) ctx->tune.align = atoi(al);
   *out = ctx;
@@ -142,6 +140,8 @@ const char* wgcs_strerror(int status) {
     case WGCS_ERR_OUT_OF_RANGE: return "slice bounds out of range";
     case WGCS_ERR_BATCH_FULL: return "staging batch full";
     case WGCS_ERR_NOT_READY: return "batch not submitted or already recycled";
+    case WGCS_ERR_CMSG: return "error parsing socket control message";
+    case WGCS_ERR_SPLIT_OVERFLOW: return "splitting coalesced packet resulted in overflow";
     case WGCS_ERR_HIP: return "HIP runtime error";
     case WGCS_ERR_NOMEM: return "out of memory";
     case WGCS_ERR_NO_DEVICE: return "no HIP device";
@@ -181,7 +181,8 @@ int wgcs_checksum_batch_host(wgcs_ctx* ctx, int mode, unsigned flags, uint8_t* h
   if (n == 0) return WGCS_OK;
   if (!h_pkts || !h_out || (!h_arena && arena_len)) return set_err(ctx, WGCS_ERR_INVALID_ARG, "NULL pointer");
   for (uint32_t i = 0; i < n; ++i) {
-    if (h_pkts[i].len >= 0x80000000u || h_pkts[i].off + h_pkts[i].len > arena_len)
+    const uint64_t off = (uint64_t)h_pkts[i].off_lo | ((uint64_t)h_pkts[i].off_hi << 32);
+    if (h_pkts[i].len >= 0x80000000u || off + h_pkts[i].len > arena_len)
       return set_err(ctx, WGCS_ERR_INVALID_ARG, "packet %u outside the arena", i);
   }
   std::lock_guard<std::mutex> g(ctx->mu);
@@ -214,7 +215,9 @@ int wgcs_checksum_batch_host(wgcs_ctx* ctx, int mode, unsigned flags, uint8_t* h
 // checksum(b, initial), tun/checksum.go:152-167
 int wgcs_checksum(wgcs_ctx* ctx, const uint8_t* b, size_t n, uint64_t initial, uint16_t* out) {
   if (!ctx || !out || (!b && n)) return WGCS_ERR_INVALID_ARG;
-  wgcs_pkt p = {0, (uint32_t)n, 0, 0, 0};
+  if (n >= 0x80000000u) return set_err(ctx, WGCS_ERR_INVALID_ARG, "buffer too large");
+  wgcs_pkt p;
+  wgcs_pkt_set(&p, 0, (uint32_t)n, 0, 0, 0, 0);
   return wgcs_checksum_batch_host(ctx, WGCS_MODE_FOLD, 0, const_cast<uint8_t*>(b), n, &p, &initial, 1, out);
 }
 
@@ -222,10 +225,14 @@ int wgcs_checksum(wgcs_ctx* ctx, const uint8_t* b, size_t n, uint64_t initial, u
 int wgcs_checksum_valid(wgcs_ctx* ctx, const uint8_t* pkt, size_t len, uint8_t iph_len, uint8_t proto, int is_v6,
                         int* valid) {
   if (!ctx || !valid || (!pkt && len)) return WGCS_ERR_INVALID_ARG;
-  if (proto != 6 && proto != 17) return set_err(ctx, WGCS_ERR_INVALID_ARG, "protocol %u", proto);
+  // pkt[srcAddrAt:...+2*addrSize] and pkt[iphLen:] (gro.go:561-562, :611); Go
+  // reaches into a slice's spare capacity for the addresses, which is not an
+  // input this ABI can see, so a packet shorter than its addresses is refused
   const size_t need = is_v6 ? 40 : 20;
   if (len < need || len < iph_len) return set_err(ctx, WGCS_ERR_OUT_OF_RANGE, "packet shorter than its addresses");
-  wgcs_pkt p = {0, (uint32_t)len, iph_len, 0, (uint8_t)((is_v6 ? WGCS_PKT_V6 : 0) | (proto == 17 ? WGCS_PKT_UDP : 0))};
+  if (len >= 0x80000000u) return set_err(ctx, WGCS_ERR_INVALID_ARG, "packet too large");
+  wgcs_pkt p;
+  wgcs_pkt_set(&p, 0, (uint32_t)len, iph_len, 0, proto, (uint8_t)(is_v6 ? WGCS_PKT_V6 : 0));
   uint8_t v = 0;
   int rc = wgcs_checksum_batch_host(ctx, WGCS_MODE_VALIDATE, 0, const_cast<uint8_t*>(pkt), len, &p, nullptr, 1, &v);
   *valid = v;
@@ -238,12 +245,9 @@ int wgcs_gso_none_checksum(wgcs_ctx* ctx, uint8_t* read_buf, size_t len, uint16_
   const uint16_t at = (uint16_t)(csum_start + csum_offset);
   if ((size_t)at + 2 > len || csum_start > len)
     return set_err(ctx, WGCS_ERR_OUT_OF_RANGE, "checksum field %u outside packet of %zu bytes", at, len);
-  if (csum_offset > 255) {
-    // wgcs_pkt carries an 8-bit offset; express the same field via csum_start
-    // is not possible in general -- such offsets never occur for TCP/UDP.
-    return set_err(ctx, WGCS_ERR_INVALID_ARG, "csum_offset %u > 255", csum_offset);
-  }
-  wgcs_pkt p = {0, (uint32_t)len, csum_start, (uint8_t)csum_offset, 0};
+  if (len >= 0x80000000u) return set_err(ctx, WGCS_ERR_INVALID_ARG, "packet too large");
+  wgcs_pkt p;
+  wgcs_pkt_set(&p, 0, (uint32_t)len, csum_start, csum_offset, 0, 0);
   uint16_t out = 0;
   return wgcs_checksum_batch_host(ctx, WGCS_MODE_PARTIAL, WGCS_F_INPLACE, read_buf, len, &p, nullptr, 1, &out);
 }

@@ -59,157 +59,20 @@ __device__ __forceinline__ uint4 ld_chunk(const uint4* p) {
   return *p;
 }
 
-// ---------------------------------------------------------------------------
-// Flat path (VALIDATE / L4_FILL, 16-lane rows): when the wave's 4 packets lie
-// back to back in the arena and each packet's summed bytes form ONE range --
-// the pseudo-header addresses directly followed by the L4 segment
-// ([12, len) for IPv4 with IHL 5, [8, len) for IPv6 without extension
-// headers; L4_FILL also skips the 2-byte checksum field) -- the wave streams
-// the 4 packets as one run: every load instruction reads 1 KiB of consecutive
-// bytes (the flat-stream access pattern) and each chunk is
-// attributed to its packet with a branch-free test.  Chunks that straddle a
-// range boundary or the field ("dirty", at most 4 per packet) contribute 0 in
-// the stream and are settled once per group, one lane per chunk.
-// Any other group (gaps, IP options, short packets) uses the row path.
-struct FlatGroup {
-  int lo[4], hi[4], hole[4];  // positions relative to the aligned run base
-  int nch;
-  const uint4* src;
+// Descriptor fields (include/wgcsum.h wgcs_pkt), unpacked from one dwordx4.
+struct Desc {
+  uint64_t off;
+  int len, cs, co, proto, flags;
 };
-
-template <int MODE, int U, bool NT>
-__device__ __forceinline__ bool flat_group(uint8_t* __restrict__ arena, const wgcs_pkt& d, uint32_t base, uint32_t n,
-                                           void* __restrict__ out, int inplace, int lane) {
-  if (base + 4 > n) return false;
-  // the 4 descriptors (row q's lane 16q holds packet base + q) as scalars
-  uint64_t off[4];
-  int len[4], cs[4], co[4], fl[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t lo32 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)d.off, 16 * q);
-    const uint32_t hi32 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(d.off >> 32), 16 * q);
-    off[q] = ((uint64_t)hi32 << 32) | lo32;
-    len[q] = __builtin_amdgcn_readlane((int)d.len, 16 * q);
-    const uint32_t w = (uint32_t)d.csum_start | ((uint32_t)d.csum_offset << 16) | ((uint32_t)d.flags << 24);
-    const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane((int)w, 16 * q);
-    cs[q] = (int)(ws & 0xFFFFu);
-    co[q] = (int)((ws >> 16) & 0xFFu);
-    fl[q] = (int)(ws >> 24);
-  }
-  int alo[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const bool v6 = (fl[q] & WGCS_PKT_V6) != 0;
-    alo[q] = v6 ? 8 : 12;
-    if (cs[q] != (v6 ? 40 : 20) || len[q] < cs[q] + 8 || len[q] > 16384) return false;
-    if (MODE == WGCS_MODE_L4_FILL && cs[q] + co[q] + 2 > len[q]) return false;
-    if (q > 0 && off[q] != off[q - 1] + (uint64_t)len[q - 1]) return false;
-  }
-  // aligned run base: the first summed byte rounded down to 16
-  uint8_t* first = arena + off[0] + alo[0];
-  const int s0 = (int)((uintptr_t)first & 15u);
-  const uint4* src = reinterpret_cast<const uint4*>(first - s0);
-  int lo[4], hi[4], hole[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int rel = (int)(off[q] - off[0]) - alo[0] + s0;  // packet start relative to the run base
-    lo[q] = rel + alo[q];
-    hi[q] = rel + len[q];
-    hole[q] = MODE == WGCS_MODE_L4_FILL ? rel + cs[q] + co[q] : -64;
-  }
-  const int nch = (hi[3] + 15) >> 4;
-  uint32_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
-  // clean chunks: all 16 bytes inside one packet's summed range (and, for
-  // L4_FILL, clear of its checksum field), summed unmasked with no divergent
-  // path; every other chunk contributes 0 here and is settled below
-  for (int c0 = 0; c0 < nch; c0 += 64 * U) {  // wave-uniform
-    uint4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int c = c0 + 64 * u + lane;
-      v[u] = c < nch ? ld_chunk<NT>(src + c) : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int x = 16 * (c0 + 64 * u + lane);
-      const bool b0 = x >= hi[0], b1 = x >= hi[1], b2 = x >= hi[2];  // packet f = b0 + b1 + b2
-      const int lo_f = b2 ? lo[3] : (b1 ? lo[2] : (b0 ? lo[1] : lo[0]));
-      const int hi_f = b2 ? hi[3] : (b1 ? hi[2] : (b0 ? hi[1] : hi[0]));
-      bool clean = x >= lo_f && x + 16 <= hi_f;  // also false past the run
-      if (MODE == WGCS_MODE_L4_FILL) {
-        const int h_f = b2 ? hole[3] : (b1 ? hole[2] : (b0 ? hole[1] : hole[0]));
-        clean = clean && (x >= h_f + 2 || x + 16 <= h_f);
-      }
-      uint32_t t = add_halves(add_halves(add_halves(add_halves(0u, v[u].x), v[u].y), v[u].z), v[u].w);
-      t = clean ? t : 0u;
-      acc0 += b0 ? 0u : t;
-      acc1 += (b0 && !b1) ? t : 0u;
-      acc2 += (b1 && !b2) ? t : 0u;
-      acc3 += b2 ? t : 0u;
-    }
-    acc0 = fold32_16(acc0);
-    acc1 = fold32_16(acc1);
-    acc2 = fold32_16(acc2);
-    acc3 = fold32_16(acc3);
-  }
-  // dirty chunks, once per group: lane 4q + s takes packet q's candidate s
-  // (its first chunk, its last chunk, the two chunks of its checksum field)
-  // unless an earlier candidate is the same chunk or the chunk is clean for q
-  // (counted above); its masked share of q goes into the lane's acc_q.  The
-  // chunk was just streamed, so the reload hits the cache.
-  {
-    const int q = (lane >> 2) & 3, sl = lane & 3;
-    const int lq = q == 0 ? lo[0] : (q == 1 ? lo[1] : (q == 2 ? lo[2] : lo[3]));
-    const int hq = q == 0 ? hi[0] : (q == 1 ? hi[1] : (q == 2 ? hi[2] : hi[3]));
-    const int hl = q == 0 ? hole[0] : (q == 1 ? hole[1] : (q == 2 ? hole[2] : hole[3]));
-    const int k0 = lq >> 4, k1 = (hq - 1) >> 4, k2 = hl >> 4, k3 = (hl + 1) >> 4;
-    const int cc = sl == 0 ? k0 : (sl == 1 ? k1 : (sl == 2 ? k2 : k3));
-    bool take = lane < 16 && (MODE == WGCS_MODE_L4_FILL || sl < 2);
-    take = take && !(sl >= 1 && cc == k0) && !(sl >= 2 && cc == k1) && !(sl == 3 && cc == k2);
-    const int x = 16 * cc;
-    bool clean = x >= lq && x + 16 <= hq;
-    if (MODE == WGCS_MODE_L4_FILL) clean = clean && (x >= hl + 2 || x + 16 <= hl);
-    if (take && !clean) {
-      const uint4 w = ld_chunk<false>(src + cc);
-      uint32_t m16 = byte_bits16(lq - x, hq - x);
-      if (MODE == WGCS_MODE_L4_FILL) m16 &= ~byte_bits16(hl - x, hl + 2 - x);
-      const uint32_t t = add_halves(add_halves(add_halves(add_halves(0u, w.x & expand_nibble(m16 & 0xFu)),
-                                                          w.y & expand_nibble((m16 >> 4) & 0xFu)),
-                                               w.z & expand_nibble((m16 >> 8) & 0xFu)),
-                                    w.w & expand_nibble((m16 >> 12) & 0xFu));
-      if (q == 0) acc0 = fold32_16(acc0 + t);
-      else if (q == 1) acc1 = fold32_16(acc1 + t);
-      else if (q == 2) acc2 = fold32_16(acc2 + t);
-      else acc3 = fold32_16(acc3 + t);
-    }
-  }
-  // per packet: wave sum, parity (pairing from the packet's first summed byte), pseudo-header constant
-  uint32_t t4[4];
-  t4[0] = fold32_16(wave_sum_u32(acc0));
-  t4[1] = fold32_16(wave_sum_u32(acc1));
-  t4[2] = fold32_16(wave_sum_u32(acc2));
-  t4[3] = fold32_16(wave_sum_u32(acc3));
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    uint32_t sq = t4[q];
-    if ((((uintptr_t)arena + off[q] + (uint64_t)alo[q]) & 1u) == 0) sq = bswap16(sq);
-    const uint32_t pre = ((fl[q] & WGCS_PKT_UDP) ? 17u : 6u) + ((uint32_t)(len[q] - cs[q]) & 0xFFFFu);
-    const uint32_t t = fold32_16(sq + pre);
-    if (lane == q) {
-      if (MODE == WGCS_MODE_VALIDATE) {
-        reinterpret_cast<uint8_t*>(out)[base + q] = (t == 0xFFFFu) ? 1 : 0;
-      } else {
-        const uint16_t cv = (uint16_t)~t;
-        reinterpret_cast<uint16_t*>(out)[base + q] = cv;
-        if (inplace) {
-          uint8_t* pkt = arena + off[q];
-          pkt[cs[q] + co[q]] = (uint8_t)(cv >> 8);
-          pkt[cs[q] + co[q] + 1] = (uint8_t)cv;
-        }
-      }
-    }
-  }
-  return true;
+__device__ __forceinline__ Desc unpack(const uint4& d) {
+  Desc r;
+  r.off = (uint64_t)d.x | ((uint64_t)(d.y & 0xFFFFu) << 32);
+  r.proto = (int)((d.y >> 16) & 0xFFu);
+  r.flags = (int)(d.y >> 24);
+  r.len = (int)d.z;
+  r.cs = (int)(d.w & 0xFFFFu);
+  r.co = (int)(d.w >> 16);
+  return r;
 }
 
 // One packet per group of G lanes (G = 16: 4 packets per wave in flight; G = 64:
@@ -219,9 +82,9 @@ __device__ __forceinline__ bool flat_group(uint8_t* __restrict__ arena, const wg
 // chunks that are summed unmasked: lanes stream interior chunk
 // c = c_lo + sub + G*(u + U*it), so one wave instruction reads 64/G
 // contiguous 16*G-byte runs, and each lane owns at most a few edge chunks.
-template <int MODE, int G, int U, bool NT, bool FLAT>
+template <int MODE, int G, int U, bool NT>
 __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict__ arena,
-                                                             const wgcs_pkt* __restrict__ pkts,
+                                                             const uint4* __restrict__ pkts,
                                                              const uint64_t* __restrict__ initial,
                                                              uint32_t n, void* __restrict__ out,
                                                              int inplace, uint32_t amask) {
@@ -233,7 +96,7 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
   const uint32_t wave =
       (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
   const uint32_t step = gridDim.x * (blockDim.x >> 6) * PPW;
-  wgcs_pkt dn = {0, 0, 0, 0, 0};
+  uint4 dn = make_uint4(0, 0, 0, 0);
   {
     const uint32_t p0 = wave * PPW + grp;
     if (p0 < n) dn = pkts[p0];
@@ -241,16 +104,13 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
   for (uint32_t base = wave * PPW; base < n; base += step) {  // wave-uniform loop
     const uint32_t p = base + grp;
     const bool active = p < n;
-    const wgcs_pkt d = dn;
+    const Desc d = unpack(dn);
     if (p + step < n) dn = pkts[p + step];  // prefetch the next descriptor
-    if constexpr (FLAT && G == 16 && (MODE == WGCS_MODE_VALIDATE || MODE == WGCS_MODE_L4_FILL)) {
-      if (flat_group<MODE, U, NT>(arena, d, base, n, out, inplace, lane)) continue;  // wave-uniform
-    }
     uint8_t* pkt = arena + d.off;
-    const int len = active ? (int)d.len : 0;
-    const int cs = d.csum_start;
-    const int co = d.csum_offset;
+    const int len = active ? d.len : 0;
+    const int cs = d.cs;
     const bool v6 = (d.flags & WGCS_PKT_V6) != 0;
+    const int fld16 = (cs + d.co) & 0xFFFF;  // u16 field position (gro.go:1391, :1503)
     Ranges r;
     r.main_lo = 0;
     r.main_hi = len;
@@ -265,11 +125,11 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
       r.main_lo = min(cs, len);
       r.addr_lo = min(v6 ? 8 : 12, len);
       r.addr_hi = min(v6 ? 40 : 20, len);
-      if (MODE == WGCS_MODE_L4_FILL) r.fld = cs + co;
-      pre = ((d.flags & WGCS_PKT_UDP) ? 17u : 6u) + ((uint32_t)(len - cs) & 0xFFFFu);
+      if (MODE == WGCS_MODE_L4_FILL) r.fld = fld16;
+      pre = (uint32_t)d.proto + ((uint32_t)(len - cs) & 0xFFFFu);  // {0, proto} + BE16(len - iphLen)
     } else if (MODE == WGCS_MODE_PARTIAL) {
       r.main_lo = min(cs, len);
-      r.fld = (cs + co) & 0xFFFF;  // u16 arithmetic, gro.go:1503
+      r.fld = fld16;
       if (r.fld + 1 < len) init = ((uint32_t)pkt[r.fld] << 8) | pkt[r.fld + 1];  // gro.go:1508
     } else {  // WGCS_MODE_IP4HDR
       r.main_hi = min(cs, len);
@@ -364,30 +224,27 @@ static hipError_t launch_mode(uint8_t* arena, const wgcs_pkt* pkts, const uint64
   long cap = (long)num_cu * t.blocks_per_cu;
   const int grid = (int)(want < cap ? want : cap);
   const uint32_t amask = (uint32_t)(t.align >= 16 ? t.align : 16) - 1u;
-#define WGCS_LAUNCH(G, U, FL)                                                                                      \
-  do {                                                                                                            \
-    if (t.nt)                                                                                                     \
-      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, true, FL>), dim3(grid), dim3(256), 0, s, arena, pkts,  \
-                         init, n, out, inplace, amask);                                                           \
-    else                                                                                                          \
-      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, false, FL>), dim3(grid), dim3(256), 0, s, arena, pkts, \
-                         init, n, out, inplace, amask);                                                           \
+  const uint4* d = reinterpret_cast<const uint4*>(pkts);
+#define WGCS_LAUNCH(G, U)                                                                                    \
+  do {                                                                                                      \
+    if (t.nt)                                                                                               \
+      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, true>), dim3(grid), dim3(256), 0, s, arena, d,  \
+                         init, n, out, inplace, amask);                                                     \
+    else                                                                                                    \
+      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, false>), dim3(grid), dim3(256), 0, s, arena, d, \
+                         init, n, out, inplace, amask);                                                     \
   } while (0)
   if (t.lanes_per_pkt == 64) {
-    if (t.unroll >= 4) WGCS_LAUNCH(64, 4, false);
-    else WGCS_LAUNCH(64, 2, false);
+    if (t.unroll >= 4) WGCS_LAUNCH(64, 4);
+    else WGCS_LAUNCH(64, 2);
   } else if (t.lanes_per_pkt == 32) {
-    if (t.unroll >= 6) WGCS_LAUNCH(32, 6, false);
-    else if (t.unroll >= 4) WGCS_LAUNCH(32, 4, false);
-    else WGCS_LAUNCH(32, 3, false);
-  } else if (t.flat && (MODE == WGCS_MODE_VALIDATE || MODE == WGCS_MODE_L4_FILL)) {
-    if (t.unroll >= 8) WGCS_LAUNCH(16, 8, true);
-    else if (t.unroll >= 6) WGCS_LAUNCH(16, 6, true);
-    else WGCS_LAUNCH(16, 4, true);
+    if (t.unroll >= 6) WGCS_LAUNCH(32, 6);
+    else if (t.unroll >= 4) WGCS_LAUNCH(32, 4);
+    else WGCS_LAUNCH(32, 3);
   } else {
-    if (t.unroll >= 8) WGCS_LAUNCH(16, 8, false);
-    else if (t.unroll >= 6) WGCS_LAUNCH(16, 6, false);
-    else WGCS_LAUNCH(16, 4, false);
+    if (t.unroll >= 8) WGCS_LAUNCH(16, 8);
+    else if (t.unroll >= 6) WGCS_LAUNCH(16, 6);
+    else WGCS_LAUNCH(16, 4);
   }
 #undef WGCS_LAUNCH
   return hipGetLastError();

@@ -349,9 +349,12 @@ struct Plan {
   uint64_t out_bytes = 0;
 };
 
-void make_plan(Planner& P, const std::vector<int>& cand, const std::vector<uint64_t>& stage_off, Plan& out) {
-  const int n = P.n;
-  for (int i = 0; i < n; ++i) {
+// raw: the loop stopped at packet `n_eff` with "invalid offset" (gro.go:1335-
+// 1337): no apply* runs, so every buffer whose bytes the coalescing changed
+// (appends, prepend swaps, PSH) becomes a RAW item holding exactly those bytes.
+void make_plan(Planner& P, const std::vector<int>& cand, const std::vector<uint64_t>& stage_off, int n_eff, bool raw,
+               Plan& out) {
+  for (int i = 0; i < n_eff; ++i) {
     int res = NOOP;
     switch (cand[i]) {
       case TCP4: res = P.tcp_gro(i, false); break;
@@ -362,40 +365,47 @@ void make_plan(Planner& P, const std::vector<int>& cand, const std::vector<uint6
     if (res == NOOP) out.zero_hdr.push_back(i);  // gro.go:1350-1358
     if (res == NOOP || res == INSERT) out.to_write.push_back(i);
   }
+  auto emit = [&](int slot, const Item& it, bool udp, bool raw_item) {
+    const Content& c = P.content[slot];
+    GroItem gi;
+    memset(&gi, 0, sizeof gi);
+    gi.out_off = out.out_bytes;
+    gi.head_off = (uint32_t)stage_off[c.pieces[0].pkt];
+    gi.pkt_len = (uint32_t)(P.lens[slot] - P.offset);
+    gi.iph = it.iph;
+    gi.l4h = it.l4h;
+    gi.gso_size = it.gso_size;
+    gi.kind = (uint8_t)((it.key.v6 ? GRO_KIND_V6 : 0) | (udp ? GRO_KIND_UDP : 0) | (c.psh ? GRO_KIND_PSH : 0) |
+                        (raw_item ? GRO_KIND_RAW : 0));
+    gi.seg_first = (uint32_t)out.segs.size();
+    const uint32_t hdr = (uint32_t)it.iph + it.l4h;
+    uint64_t dst = out.out_bytes + kVnetLen + hdr;
+    for (size_t k = 0; k < c.pieces.size(); ++k) {  // piece 0 = head packet; its header is rebuilt
+      Piece pc = c.pieces[k];
+      if (k == 0) {
+        pc.start += hdr;
+        pc.len -= hdr;
+      }
+      if (pc.len) out.segs.push_back({(uint32_t)(stage_off[pc.pkt] + pc.start), pc.len, (uint32_t)dst, 0u});
+      dst += pc.len;
+    }
+    gi.seg_count = (uint32_t)out.segs.size() - gi.seg_first;
+    out.items.push_back(gi);
+    out.item_slot.push_back(slot);
+    out.out_bytes += (kVnetLen + gi.pkt_len + 15) & ~(uint64_t)15;
+  };
   auto apply = [&](std::unordered_map<FlowKey, std::vector<Item>, FlowHash>& table, bool udp) {
     for (auto& kv : table) {
       for (const Item& it : kv.second) {
         const int slot = it.bufs_index;
-        if (it.num_merged == 0) {
-          out.zero_hdr.push_back(slot);
-          continue;
-        }
         const Content& c = P.content[slot];
-        GroItem gi;
-        memset(&gi, 0, sizeof gi);
-        gi.out_off = out.out_bytes;
-        gi.head_off = (uint32_t)stage_off[c.pieces[0].pkt];
-        gi.pkt_len = (uint32_t)(P.lens[slot] - P.offset);
-        gi.iph = it.iph;
-        gi.l4h = it.l4h;
-        gi.gso_size = it.gso_size;
-        gi.kind = (uint8_t)((it.key.v6 ? GRO_KIND_V6 : 0) | (udp ? GRO_KIND_UDP : 0) | (c.psh ? GRO_KIND_PSH : 0));
-        gi.seg_first = (uint32_t)out.segs.size();
-        const uint32_t hdr = (uint32_t)it.iph + it.l4h;
-        uint64_t dst = out.out_bytes + kVnetLen + hdr;
-        for (size_t k = 0; k < c.pieces.size(); ++k) {  // piece 0 = head packet; its header is rebuilt
-          Piece pc = c.pieces[k];
-          if (k == 0) {
-            pc.start += hdr;
-            pc.len -= hdr;
-          }
-          if (pc.len) out.segs.push_back({(uint32_t)(stage_off[pc.pkt] + pc.start), pc.len, (uint32_t)dst, 0u});
-          dst += pc.len;
+        if (raw) {
+          if (c.pieces.size() > 1 || c.psh) emit(slot, it, udp, true);
+        } else if (it.num_merged == 0) {
+          out.zero_hdr.push_back(slot);
+        } else {
+          emit(slot, it, udp, false);
         }
-        gi.seg_count = (uint32_t)out.segs.size() - gi.seg_first;
-        out.items.push_back(gi);
-        out.item_slot.push_back(slot);
-        out.out_bytes += (kVnetLen + gi.pkt_len + 15) & ~(uint64_t)15;
       }
     }
   };
@@ -408,7 +418,7 @@ void init_planner(Planner& P, uint8_t** bufs, size_t* lens, size_t* caps, int n,
   P.bufs = bufs;
   P.lens = lens;
   P.caps = caps;
-  P.n = n;
+  P.n = n;  // packets the loop reaches
   P.offset = offset;
   P.orig = orig;
   P.valid = valid;
@@ -449,17 +459,23 @@ extern "C" int wgcs_handle_gro(wgcs_ctx* ctx, uint8_t** bufs, size_t* lens, size
   if (!ctx || !n_to_write || (n > 0 && (!bufs || !lens || !caps || !to_write))) return WGCS_ERR_INVALID_ARG;
   *n_to_write = 0;
   if (n <= 0) return WGCS_OK;
-  for (int i = 0; i < n; ++i)  // gro.go:1335-1337 (checked up front: no partial mutation)
-    if (offset < kVnetLen || (long)offset > (long)lens[i] - 1)
-      return set_err(ctx, WGCS_ERR_INVALID_OFFSET, "invalid offset (packet %d)", i);
+  // gro.go:1335-1337: the loop returns "invalid offset" at the first bad
+  // buffer, after the earlier ones went through tcpGRO / udpGRO
+  int n_eff = n;
+  for (int i = 0; i < n; ++i)
+    if (offset < kVnetLen || (long)offset > (long)lens[i] - 1) {
+      n_eff = i;
+      break;
+    }
+  const bool bad_offset = n_eff < n;
 
-  std::vector<const uint8_t*> orig(n);
-  std::vector<int> cand(n);
+  std::vector<const uint8_t*> orig(n, nullptr);
+  std::vector<int> cand(n, NOT_CAND);
   std::vector<uint64_t> stage_off(n, 0);
   std::vector<uint8_t> assume(n, 0);
   uint64_t stage_bytes = 0;
   uint32_t ncand = 0;
-  for (int i = 0; i < n; ++i) {
+  for (int i = 0; i < n_eff; ++i) {
     orig[i] = bufs[i] + offset;
     cand[i] = gro_candidate(orig[i], lens[i] - offset, can_udp_gro != 0);
     if (cand[i] != NOT_CAND) {
@@ -474,9 +490,9 @@ extern "C" int wgcs_handle_gro(wgcs_ctx* ctx, uint8_t** bufs, size_t* lens, size
   const std::vector<size_t> lens0(lens, lens + n), caps0(caps, caps + n);
 
   Planner P;
-  init_planner(P, bufs, lens, caps, n, offset, orig, assume);
+  init_planner(P, bufs, lens, caps, n_eff, offset, orig, assume);
   Plan pl;
-  make_plan(P, cand, stage_off, pl);
+  make_plan(P, cand, stage_off, n_eff, bad_offset, pl);
 
   std::lock_guard<std::mutex> g(ctx->mu);
   hipSetDevice(ctx->device);
@@ -495,18 +511,14 @@ extern "C" int wgcs_handle_gro(wgcs_ctx* ctx, uint8_t** bufs, size_t* lens, size
     uint8_t* hv = (uint8_t*)(hp + ncand);
     std::vector<int> cidx;
     cidx.reserve(ncand);
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n_eff; ++i) {
       if (cand[i] == NOT_CAND) continue;
       memcpy(hs + stage_off[i], orig[i], lens0[i] - offset);
       const bool v6 = cand[i] == TCP6 || cand[i] == UDP6;
       const bool udp = cand[i] == UDP4 || cand[i] == UDP6;
-      wgcs_pkt d;
-      d.off = stage_off[i];
-      d.len = (uint32_t)(lens0[i] - offset);
-      d.csum_start = (uint16_t)(v6 ? 40 : 20);  // item.iphLen (IHL 5 for IPv4 candidates)
-      d.csum_offset = 0;
-      d.flags = (uint8_t)((v6 ? WGCS_PKT_V6 : 0) | (udp ? WGCS_PKT_UDP : 0));
-      hp[cidx.size()] = d;
+      // checksumValid(pkt, item.iphLen (IHL 5 for IPv4 candidates), proto, isV6)
+      wgcs_pkt_set(&hp[cidx.size()], stage_off[i], (uint32_t)(lens0[i] - offset), (uint16_t)(v6 ? 40 : 20), 0,
+                   (uint8_t)(udp ? 17 : 6), (uint8_t)(v6 ? WGCS_PKT_V6 : 0));
       cidx.push_back(i);
     }
     hipError_t e = hipMemcpyAsync(ctx->d_arena.ptr, hs, stage_bytes, hipMemcpyHostToDevice, s);
@@ -520,28 +532,32 @@ extern "C" int wgcs_handle_gro(wgcs_ctx* ctx, uint8_t** bufs, size_t* lens, size
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "GRO sync");
     for (uint32_t k = 0; k < ncand; ++k) real[cidx[k]] = hv[k];
     bool redo = false;
-    for (int i = 0; i < n && !redo; ++i) redo = P.consulted[i] && !real[i];
+    for (int i = 0; i < n_eff && !redo; ++i) redo = P.consulted[i] && !real[i];
     if (redo) {  // mis-speculated: restore the slice headers, plan with the real bits
       std::copy(bufs0.begin(), bufs0.end(), bufs);
       std::copy(lens0.begin(), lens0.end(), lens);
       std::copy(caps0.begin(), caps0.end(), caps);
       Planner Q;
-      init_planner(Q, bufs, lens, caps, n, offset, orig, real);
+      init_planner(Q, bufs, lens, caps, n_eff, offset, orig, real);
       pl = Plan();
-      make_plan(Q, cand, stage_off, pl);
+      make_plan(Q, cand, stage_off, n_eff, bad_offset, pl);
       if ((rc = queue_coalesce(ctx, pl, s))) return rc;
       if (!pl.items.empty() && (e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "GRO sync");
     }
   }
 
-  // ---- apply: empty virtio headers, coalesced super-packets, toWrite
+  // ---- apply: empty virtio headers, coalesced super-packets (or, after an
+  // invalid offset, the raw coalesced bytes), toWrite
   static const uint8_t zero_hdr[kVnetLen] = {0};
   for (int slot : pl.zero_hdr) memcpy(bufs[slot] + offset - kVnetLen, zero_hdr, kVnetLen);
   for (size_t k = 0; k < pl.items.size(); ++k) {
     const int slot = pl.item_slot[k];
-    memcpy(bufs[slot] + offset - kVnetLen, (uint8_t*)ctx->h_out.ptr + pl.items[k].out_off,
-           kVnetLen + pl.items[k].pkt_len);
+    const GroItem& it = pl.items[k];
+    if (it.kind & GRO_KIND_RAW)
+      memcpy(bufs[slot] + offset, (uint8_t*)ctx->h_out.ptr + it.out_off + kVnetLen, it.pkt_len);
+    else
+      memcpy(bufs[slot] + offset - kVnetLen, (uint8_t*)ctx->h_out.ptr + it.out_off, kVnetLen + it.pkt_len);
   }
   for (int i : pl.to_write) to_write[(*n_to_write)++] = i;
-  return WGCS_OK;
+  return bad_offset ? set_err(ctx, WGCS_ERR_INVALID_OFFSET, "invalid offset (packet %d)", n_eff) : WGCS_OK;
 }

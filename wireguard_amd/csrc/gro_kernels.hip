@@ -82,6 +82,14 @@ __global__ __launch_bounds__(256) void gro_coalesce_kernel(const uint8_t* __rest
     h.csum_at = g.iph + (h.udp ? 6 : 16);
     h.pkt_len = g.pkt_len;
     uint8_t* o = out + g.out_off;
+    if (g.kind & GRO_KIND_RAW) {  // coalesced, never applied (gro.go:1335-1337 returned first)
+      for (int x = lane; x < h.hdr_len; x += 64) {
+        uint32_t b = head[x];
+        if (!h.udp && h.psh && x == h.iph + 13) b |= 0x08;  // PSH (gro.go:724-729)
+        o[10 + x] = (uint8_t)b;
+      }
+      return;
+    }
     // IPv4 header checksum: ^checksum(pkt[:iphLen], 0) after the patches
     uint32_t ipw = 0, adw = 0;
     const int a_lo = h.v6 ? 8 : 12, a_hi = h.v6 ? 40 : 20;

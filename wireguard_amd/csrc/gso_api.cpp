@@ -42,9 +42,18 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   if (buf_lens[0] < (size_t)offset) return set_err(ctx, WGCS_ERR_OUT_OF_RANGE, "offset beyond bufs[0]");
   const size_t room = std::min<size_t>(buf_lens[0] - (size_t)offset, 0xFFFFFFFFu);
   uint32_t pitch, nseg_bound;
-  gso_out_layout(vbuf, vlen, (uint32_t)nbufs, &pitch, &nseg_bound);
+  gso_out_layout(vbuf, vlen, jflags, (uint32_t)nbufs, &pitch, &nseg_bound);
   if (pitch == 0) pitch = 16;
   const size_t region = (size_t)pitch * nseg_bound;
+  // header geometry as the kernel will see it (for the per-buffer slice checks)
+  const bool raw = (jflags & WGCS_GSO_JOB_RAW) != 0;
+  uint8_t gtype = vlen >= 10 ? vbuf[1] : 0;
+  uint16_t cs = 0;
+  if (vlen >= 10) memcpy(&cs, vbuf + 6, 2);
+  const bool v4 = raw ? (jflags & WGCS_GSO_JOB_V6) == 0 : (vlen > 10 && (vbuf[10] >> 4) == 4);
+  // An IPv4 header shorter than 6 bytes makes the id update read bufs[i]'s own
+  // bytes 4-5 (gro.go:1427): the kernel reads them from the segment's slot.
+  const bool stale_id = (raw || gtype != 0) && v4 && cs <= 5 && region;
   hipSetDevice(ctx->device);
   int rc;
   const size_t meta = (size_t)nbufs * 4 + 16;  // sizes[nbufs] | count | status
@@ -68,6 +77,13 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   int32_t* d_status = d_count + 1;
   hipError_t e = hipMemcpyAsync(ctx->d_arena.ptr, vbuf, vlen, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->d_aux.ptr, hjob, aux, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && stale_id) {
+    uint8_t* hs = (uint8_t*)ctx->h_stage.ptr;
+    memset(hs, 0, region);
+    for (uint32_t i = 0; i < nseg_bound && i < (uint32_t)nbufs; ++i)
+      if (buf_lens[i] > (size_t)offset) memcpy(hs + (size_t)i * pitch, bufs[i] + offset, std::min<size_t>(6, buf_lens[i] - offset));
+    e = hipMemcpyAsync(ctx->d_out.ptr, hs, region, hipMemcpyHostToDevice, s);
+  }
   if (e != hipSuccess) return hip_fail(ctx, e, "H2D");
   e = launch_gso_split_batch((const uint8_t*)ctx->d_arena.ptr, (const wgcs_gso_job*)ctx->d_aux.ptr, 1,
                              (uint8_t*)ctx->d_out.ptr, 0, 0, (uint32_t)nbufs, d_sizes, d_count, d_status, s,
@@ -87,7 +103,9 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   const int written = res->status == WGCS_ERR_TOO_MANY_SEGMENTS ? nbufs : res->count;
   for (int i = 0; i < written; ++i) {
     sizes[i] = h[i];
-    if (buf_lens[i] < (size_t)offset + (size_t)h[i]) {  // the Go code would panic on this slice
+    const bool last = res->status == 0 && i == written - 1;
+    const size_t need = gso_split_need(vbuf, vlen, jflags, (size_t)h[i], last);
+    if (buf_lens[i] < (size_t)offset + need) {  // the Go code would panic on this slice
       res->status = WGCS_ERR_OUT_OF_RANGE;
       res->count = i;
       return WGCS_OK;

@@ -32,28 +32,6 @@
 #include "wgcs_rows.h"
 #include "wgcs_kernels.h"
 
-// Timing-experiment knobs (scripts/exp_gso.sh builds variants into exp/);
-// the product library is always built with WGCS_GSO_EXP = 0.
-#ifndef WGCS_GSO_EXP
-#define WGCS_GSO_EXP 0
-#endif
-#if WGCS_GSO_EXP & 64
-__device__ unsigned long long g_gso_stamps[1 << 16];
-#define GSO_STAMP(k)                                                                                         \
-  do {                                                                                                       \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                              \
-    if ((threadIdx.x & 63) == 0)                                                                             \
-      g_gso_stamps[(((blockIdx.y * gridDim.x + blockIdx.x) * 16 + (threadIdx.x >> 6)) * 8 + (k)) & 0xFFFF] = t_; \
-  } while (0)
-extern "C" int wgcs_exp_stamps(void* host, size_t bytes) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gso_stamps), bytes, 0, hipMemcpyDeviceToHost);
-}
-#else
-#define GSO_STAMP(k) \
-  do {               \
-  } while (0)
-#endif
-
 namespace wgcs {
 
 namespace {
@@ -108,16 +86,30 @@ struct Job {
   int count;     // return value n
   int type, flags, ipv;
   int hdr_len, gso, cs, co, plen;
+  int gen;       // 1: byte-granular general path (gso_general_row); 0: the row-streaming fast path
 };
+
+// Bytes of bufs[i][offset:] one gsoSplit segment writes (gro.go:1419-1488,
+// oracle or_gso_split_need): the packet plus fixed-position header writes that
+// may lie past it (IPv4 [2:12), IPv6 [4:6), seq / UDP length at csumStart+4,
+// the flags byte on non-last segments, the checksum field; u16 positions).
+__device__ __forceinline__ int split_need(const Job& j, int pkt_len, bool any_non_last) {
+  const bool tcp = j.type != GSO_UDP_L4;
+  int need = max(pkt_len, j.ipv == 4 ? 12 : 6);
+  need = max(need, ((j.cs + 4) & 0xFFFF) + (tcp ? 4 : 2));
+  if (tcp && any_non_last) need = max(need, ((j.cs + 13) & 0xFFFF) + 1);
+  return max(need, ((j.cs + j.co) & 0xFFFF) + 2);
+}
 
 // Segment count / ErrTooManySegments (gro.go:1406-1410) + output room.
 __device__ void count_segments(Job& j, uint32_t out_room, uint32_t max_segs) {
   const int plen = j.plen;
   long nseg = 0;
   if (j.hdr_len < plen) nseg = j.gso == 0 ? 0x7FFFFFFF : ((long)plen - j.hdr_len + j.gso - 1) / j.gso;
-  if (nseg > 0) {
+  if (nseg > 0) {  // segment 0 is the largest; Go panics on a bufs[0] slice shorter than what it writes
     const int first = j.hdr_len + min(j.gso, plen - j.hdr_len);
-    if ((uint32_t)first > out_room) { j.status = WGCS_ERR_OUT_OF_RANGE; return; }
+    const bool non_last = nseg > 1;
+    if ((uint32_t)split_need(j, first, non_last) > out_room) { j.status = WGCS_ERR_OUT_OF_RANGE; return; }
   }
   if (nseg > (long)max_segs) {  // gro.go:1409-1410: all bufs written, n = i - 1
     j.nseg = (int)max_segs;
@@ -129,20 +121,29 @@ __device__ void count_segments(Job& j, uint32_t out_room, uint32_t max_segs) {
   }
 }
 
-// gsoSplit's own slice bounds (gro.go:1388-1402,:1419,:1442,:1474-1475) and
-// this kernel's header limits (Linux never produces violating TCP/UDP GSO
-// headers).
-__device__ bool split_bounds_ok(const Job& j) {
+// gsoSplit's own bounds (gro.go:1387-1405 before the loop; :1419-1478 once it
+// runs): an index the Go code would panic on is OUT_OF_RANGE.  Every position
+// is the reference's uint16 sum.  Pseudo-header addresses past len(readBuf)
+// (Go's spare capacity) are refused as well.  Then: does the
+// job fit the row-streaming path (header <= 240 bytes, IP header at least the
+// fixed IPv4 / IPv6 size, checksum field inside the header), or does it take
+// the byte-granular general path?
+__device__ bool split_bounds(Job& j) {
   const int plen = j.plen;
-  const int csum_at = (j.cs + j.co) & 0xFFFF;
-  const bool tcp = j.type != GSO_UDP_L4;
-  if (j.cs > plen || j.hdr_len < j.cs || csum_at + 2 > plen || (tcp && j.cs + 8 > plen)) return false;
-  if (j.ipv == 4 ? (plen < 20 || j.cs < 20) : (plen < 40 || j.cs < 40)) return false;
-  if (csum_at + 2 > j.hdr_len || j.hdr_len > kMaxHdrLen) return false;
+  const bool v4 = j.ipv == 4, tcp = j.type != GSO_UDP_L4;
+  const int ca = (j.cs + j.co) & 0xFFFF;
+  if (v4 && plen < 12) return false;                           // readBuf[10], [11]
+  if (ca + 2 > plen) return false;                             // readBuf[checksumAt+1]
+  if (tcp && ((j.cs + 4) & 0xFFFF) + 4 > plen) return false;   // Uint32(readBuf[csumStart+4:])
+  if (j.hdr_len < plen) {                                      // the loop runs
+    if (j.cs > j.hdr_len) return false;                        // pkt[csumStart:hdrLen]
+    if (plen < (v4 ? 20 : 40)) return false;                   // address slices
+  }
+  j.gen = !(j.cs >= (v4 ? 20 : 40) && ca + 2 <= j.hdr_len && j.hdr_len <= kMaxHdrLen);
   return true;
 }
 
-// handleVirtioRead's checks (tun/tun.go:522-630) + this kernel's limits.
+// handleVirtioRead's checks (tun/tun.go:522-630), then gsoSplit's.
 __device__ Job decode_job(const HdrBytes& hb, uint32_t len, uint32_t jflags, uint32_t out_room, uint32_t max_segs) {
   Job j = {};
   if (len < 10) { j.status = WGCS_ERR_SHORT_BUFFER; return j; }  // gro.go:84-86
@@ -157,13 +158,10 @@ __device__ Job decode_job(const HdrBytes& hb, uint32_t len, uint32_t jflags, uin
   if (jflags & WGCS_GSO_JOB_RAW) {  // gsoSplit with the caller's header (gro.go:1373)
     j.ipv = (jflags & WGCS_GSO_JOB_V6) ? 6 : 4;
     if (j.type != GSO_TCPV4 && j.type != GSO_TCPV6) j.type = GSO_UDP_L4;  // protocol choice :1398-1405
-    if (!split_bounds_ok(j)) { j.status = WGCS_ERR_OUT_OF_RANGE; return j; }
+    if (!split_bounds(j)) { j.status = WGCS_ERR_OUT_OF_RANGE; return j; }
     count_segments(j, out_room, max_segs);
     return j;
   }
-#if WGCS_GSO_EXP & 64
-  GSO_STAMP(2);  // virtio fields and the job flags read
-#endif
   if (j.type == GSO_NONE) {  // tun/tun.go:532-556
     if (j.flags & 1) {
       const int at = (j.cs + j.co) & 0xFFFF;
@@ -200,11 +198,140 @@ __device__ Job decode_job(const HdrBytes& hb, uint32_t len, uint32_t jflags, uin
   if (plen < j.hdr_len) { j.status = WGCS_ERR_HDR_LEN; return j; }               // :615-621
   const int csum_at = (j.cs + j.co) & 0xFFFF;
   if (csum_at + 1 >= plen) { j.status = WGCS_ERR_CSUM_OFFSET; return j; }        // :622-630
-  if (!split_bounds_ok(j)) { j.status = WGCS_ERR_OUT_OF_RANGE; return j; }
+  if (!split_bounds(j)) { j.status = WGCS_ERR_OUT_OF_RANGE; return j; }
   count_segments(j, out_room, max_segs);
   return j;
 }
 
+// ---------------------------------------------------------------------------
+// General path: one 16-lane row per segment, byte-granular, for every header
+// geometry the reference accepts that the row-streaming path does not take
+// (IP headers shorter than 20 / 40 bytes, headers over 240 bytes, checksum
+// fields outside the header or wrapped past 2^16).  Each output byte is the
+// last value gsoSplit's write sequence leaves at its position
+// (gro.go:1419-1488, in order: IP header copy, id / length / IPv4 checksum,
+// L4 header copy, seq + flags or UDP length, payload, L4 checksum), computed
+// from readBuf with its zeroed fields (:1388, :1393).  Three passes over the
+// segment's chunks: IPv4 header sum, L4 sum, store.
+struct GenSeg {
+  const uint8_t* rb;
+  int plen, cs, hdr_len, ca, s4, f13, i;
+  int seg_start, pkt_len;
+  bool v4, tcp, last;
+  uint32_t id45;    // IPv4 bytes 4-5 after the id step (i > 0: BE16 + 1)
+  uint32_t seq, ulen;
+  uint32_t ipc;     // IPv4 header checksum (bytes 10-11)
+};
+
+// readBuf byte x after gsoSplit zeroed its IPv4 checksum and L4 checksum fields
+__device__ __forceinline__ uint32_t rbz(const GenSeg& g, int x) {
+  if ((g.v4 && (x == 10 || x == 11)) || x == g.ca || x == g.ca + 1) return 0u;
+  return g.rb[x];
+}
+
+// byte x of the IP header after the id / length writes (x < csumStart = iphLen)
+__device__ __forceinline__ uint32_t ip_stage(const GenSeg& g, int x) {
+  if (g.v4) {
+    if (x == 2) return ((uint32_t)g.pkt_len >> 8) & 0xFFu;
+    if (x == 3) return (uint32_t)g.pkt_len & 0xFFu;
+    if (x == 4) return g.id45 >> 8;
+    if (x == 5) return g.id45 & 0xFFu;
+  } else {
+    const uint32_t pl = (uint32_t)(g.pkt_len - g.cs) & 0xFFFFu;  // :1439
+    if (x == 4) return pl >> 8;
+    if (x == 5) return pl & 0xFFu;
+  }
+  return rbz(g, x);
+}
+
+// byte x (< pkt_len) before the L4 checksum store
+__device__ __forceinline__ uint32_t pre_csum(const GenSeg& g, int x) {
+  if (x >= g.hdr_len) return rbz(g, g.seg_start + (x - g.hdr_len));  // payload (:1468)
+  const int t = x - g.s4;
+  if (g.tcp && t >= 0 && t < 4) return (g.seq >> (24 - 8 * t)) & 0xFFu;
+  if (!g.tcp && t >= 0 && t < 2) return (g.ulen >> (8 - 8 * t)) & 0xFFu;
+  uint32_t b;
+  if (x >= g.cs) b = rbz(g, x);
+  else if (g.v4 && x == 10) b = g.ipc >> 8;
+  else if (g.v4 && x == 11) b = g.ipc & 0xFFu;
+  else b = ip_stage(g, x);
+  if (g.tcp && !g.last && x == g.f13) b &= ~0x09u;  // FIN|PSH (:1447-1459)
+  return b;
+}
+
+// One segment on one 16-lane row (lane r): the three passes, then sizes[].
+__device__ void gso_general_row(const uint8_t* rb, int plen, int type, int ipv, int hdr_len, int gso, int cs, int co,
+                                int i, uint8_t* dst, int r, int32_t* size_out) {
+  GenSeg g;
+  g.rb = rb;
+  g.plen = plen;
+  g.cs = cs;
+  g.hdr_len = hdr_len;
+  g.v4 = ipv == 4;
+  g.tcp = type != GSO_UDP_L4;
+  g.ca = (cs + co) & 0xFFFF;
+  g.s4 = (cs + 4) & 0xFFFF;
+  g.f13 = (cs + 13) & 0xFFFF;
+  g.i = i;
+  g.seg_start = hdr_len + i * gso;
+  const int seg_end = min(plen, g.seg_start + gso);
+  const int seg_len = seg_end - g.seg_start;
+  g.pkt_len = hdr_len + seg_len;
+  g.last = seg_end == plen;
+  g.seq = 0;
+  if (g.tcp) {  // firstSeq from the zeroed readBuf (:1402), u16 product (:1445)
+    const uint32_t s0 = (rbz(g, g.s4) << 24) | (rbz(g, g.s4 + 1) << 16) | (rbz(g, g.s4 + 2) << 8) | rbz(g, g.s4 + 3);
+    g.seq = s0 + (uint32_t)(uint16_t)((uint16_t)gso * (uint16_t)i);
+  }
+  g.ulen = (uint32_t)(uint16_t)(seg_len + (hdr_len - cs));  // :1462-1465
+  g.id45 = 0;
+  if (g.v4) {  // pkt[4:6] after copy(pkt, readBuf[:iphLen]); bytes past iphLen are what bufs[i] held (:1427)
+    const uint32_t b4 = 4 < cs ? rbz(g, 4) : (uint32_t)dst[4];
+    const uint32_t b5 = 5 < cs ? rbz(g, 5) : (uint32_t)dst[5];
+    g.id45 = (b4 << 8) | b5;
+    if (i > 0) g.id45 = (g.id45 + 1) & 0xFFFFu;  // quirk: id0 + 1 (:1426-1431)
+  }
+  // pass 1: IPv4 header checksum over pkt[:iphLen] after the id / length writes (:1434)
+  g.ipc = 0;
+  const int dalign = (int)((uintptr_t)dst & 15u);
+  uint8_t* dbase = dst - dalign;
+  if (g.v4) {
+    uint64_t acc = 0;
+    for (int x = r; x < cs; x += 16) acc += (uint64_t)ip_stage(g, x) << ((x & 1) ? 0 : 8);
+    const uint32_t t = fold32_16(row16_sum_u32(fold64_16(acc)));
+    g.ipc = (~t) & 0xFFFFu;
+  }
+  // pass 2: L4 sum over pkt[csumStart:pktLen] + the pseudo header (:1469-1483)
+  uint64_t acc = 0;
+  for (int x = cs + r; x < g.pkt_len; x += 16) acc += (uint64_t)pre_csum(g, x) << (((x - cs) & 1) ? 0 : 8);
+  {
+    const int a_lo = g.v4 ? 12 : 8, a_n = g.v4 ? 4 : 16;  // address words (readBuf, zeroed fields)
+    if (r < a_n) acc += (rbz(g, a_lo + 2 * r) << 8) | rbz(g, a_lo + 2 * r + 1);
+  }
+  const uint32_t tlen = (uint32_t)(uint16_t)(hdr_len - cs + seg_len);
+  uint32_t t = fold32_16(row16_sum_u32(fold64_16(acc)));
+  t = fold32_16(t + (g.tcp ? 6u : 17u) + tlen);
+  const uint32_t l4c = (~t) & 0xFFFFu;
+  // pass 3: every byte of the packet, the checksum last (:1485-1488)
+  const int nk = (g.pkt_len + dalign + 15) >> 4;
+  for (int k = r; k < nk; k += 16) {
+    const int x0 = 16 * k - dalign;
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const int x = x0 + b;
+      uint32_t v = 0;
+      if (x >= 0 && x < g.pkt_len) {
+        if (x == g.ca) v = l4c >> 8;
+        else if (x == g.ca + 1) v = l4c & 0xFFu;
+        else v = pre_csum(g, x);
+      }
+      w[b >> 2] |= v << (8 * (b & 3));
+    }
+    store_chunk(dbase + 16 * k, make_uint4(w[0], w[1], w[2], w[3]), x0, g.pkt_len);
+  }
+  if (r == 0) *size_out = g.pkt_len;
+}
 // gsoNoneChecksum + copy to bufs[0] (tun/tun.go:532-556, gro.go:1497-1517).
 __device__ void none_segment(const uint8_t* rb, const Job& j, uint8_t* dst, int lane) {
   const int plen = j.plen;
@@ -323,7 +450,7 @@ __device__ __forceinline__ HdrFast header_fast(const HdrBytes& hb, const Job& j,
   const int cs = j.cs, hl = j.hdr_len, ca = (j.cs + j.co) & 0xFFFF;
   const bool v4 = j.ipv == 4, tcp = j.type != GSO_UDP_L4;
   const int vlo = cs + 4, vhi = tcp ? cs + 8 : cs + 6;  // per-segment L4 field bytes
-  h.fast = (tcp ? cs + 14 <= hl : vhi <= hl) && (ca + 2 <= vlo || ca >= vhi) &&
+  h.fast = (tcp ? cs + 14 <= hl : vhi <= hl) && (ca + 2 <= vlo || ca >= vhi) && ca >= cs &&
            (!tcp || (ca != cs + 13 && ca + 1 != cs + 13));
   const int a_lo = v4 ? 12 : 8, a_hi = v4 ? 20 : 40;
   uint32_t ip = 0, l4 = 0, ad = 0;
@@ -372,7 +499,7 @@ __device__ __forceinline__ void put_be16_u(uint4& P, int r, int pos, uint32_t va
 
 // Job-level values decoded once per block by wave 0 and broadcast through LDS.
 struct JobInfo {
-  int32_t status, count, nseg, type, ipv, hdr_len, gso, cs, co, plen, flags, fast;
+  int32_t status, count, nseg, type, ipv, hdr_len, gso, cs, co, plen, flags, fast, gen;
   uint32_t id0, seq0, ip_base, l4_base, addr, tflags;
 };
 
@@ -397,7 +524,6 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   const int r = lane & 15;
   const int wv = threadIdx.x >> 6;
   const uint32_t jb = blockIdx.x;
-  GSO_STAMP(0);
   const wgcs_gso_job job = jobs[jb];  // one scalar load of the whole descriptor, flags included
   const uint8_t* vb = arena + job.off;
   const uint32_t jlen = job.len;
@@ -430,10 +556,6 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   if (wv == kDec) {
     __builtin_amdgcn_s_setprio(3);  // the decode chain is the block's critical path (until barrier 2)
     hb.load(vb, (int)min(jlen, 256u), lane);
-#if WGCS_GSO_EXP & 64
-    if (__builtin_amdgcn_readfirstlane((int)(hb.r0 + hb.r3)) == -1) hb.r1 = 0;  // stamp 5: header bytes arrived
-    GSO_STAMP(5);
-#endif
     jd = decode_job(hb, jlen, job.flags, room, max_segs);
     jd_ok = jd.status == 0 || jd.status == WGCS_ERR_TOO_MANY_SEGMENTS;
     if (lane == 0) {
@@ -448,14 +570,12 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
       ji.co = jd.co;
       ji.plen = jd.plen;
       ji.flags = jd.flags;
+      ji.gen = jd.gen;
       if (blockIdx.y == 0) {
         count[jb] = ji.count;
         status[jb] = jd.status;
       }
     }
-#if WGCS_GSO_EXP & 64
-    GSO_STAMP(6);
-#endif
   }
 
   // ---- speculative first payload batch.  The source window of segment i
@@ -512,13 +632,17 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   uint4 H1 = ld_src<NT>(spec ? (hab_s + 16 < hend_s ? hab_s + 16 : hsafe) : hdummy);
 
   lds_barrier();  // barrier 1: geometry; the speculative loads stay in flight
-  GSO_STAMP(1);
   // block-uniform: whether the header phase (and so barrier 2) happens at all
-  const bool hdr_phase = ufl(ji.nseg) > 0 && ufl(ji.type) != GSO_NONE;
+  const bool hdr_phase = ufl(ji.nseg) > 0 && ufl(ji.type) != GSO_NONE && ufl(ji.gen) == 0;
   if (wv == kDec && hdr_phase) {
     const HdrFast hf = header_fast(hb, jd, lane);
-    const uint32_t id0 = jd.ipv == 4 ? hb.be16(10 + 4) : 0u;
-    const uint32_t seq0 = jd.type != GSO_UDP_L4 ? hb.be32(10 + jd.cs + 4) : 0u;
+    // readBuf bytes after gsoSplit zeroed the L4 checksum field (gro.go:1393;
+    // the IPv4 checksum bytes 10-11 are neither id nor seq here: cs >= 20)
+    const int ca = (jd.cs + jd.co) & 0xFFFF;
+    auto zb = [&](int x) { return (x == ca || x == ca + 1) ? 0u : hb(10 + x); };
+    const uint32_t id0 = jd.ipv == 4 ? (zb(4) << 8) | zb(5) : 0u;
+    const int sq = jd.cs + 4;
+    const uint32_t seq0 = jd.type != GSO_UDP_L4 ? (zb(sq) << 24) | (zb(sq + 1) << 16) | (zb(sq + 2) << 8) | zb(sq + 3) : 0u;
     if (lane == 0) {
       ji.fast = hf.fast ? 1 : 0;
       ji.id0 = id0;
@@ -528,9 +652,6 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
       ji.addr = hf.addr;
       ji.tflags = hf.flags;
     }
-#if WGCS_GSO_EXP & 64
-    GSO_STAMP(7);
-#endif
     // barrier 2 (header constants).  Waves that retire early are not waited
     // for: s_barrier only counts the workgroup's surviving waves.
     lds_barrier();
@@ -558,6 +679,10 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   j.gso = ufl(ji.gso);
   const bool v4 = j.ipv == 4, tcp = j.type != GSO_UDP_L4;
   if (i >= j.nseg) return;  // whole rows retire; DPP below stays inside live rows
+  if (ufl(ji.gen)) {  // block-uniform: no barrier 2 for general jobs
+    gso_general_row(rb, j.plen, j.type, j.ipv, j.hdr_len, j.gso, j.cs, j.co, i, dst, r, &sizes[slot0 + (uint32_t)i]);
+    return;
+  }
   const bool spec_ok = spec && j.gso == gso_s;  // always true: both read virtio bytes 4-5
 
   // ---- segment geometry (row-uniform)
@@ -612,7 +737,6 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
       }
     }
   }
-  GSO_STAMP(3);
 
   // ---- lane-dense header phase (fast headers of <= 113 bytes): the row
   // publishes its payload sum and the payload part of its header chunks, and
@@ -699,7 +823,6 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
     const uint4 keep2 = s_keep[valid2 ? sloc : 0][c];
     if (valid2 && c < hk2) store_chunk(dbase2 + 16 * c, select_bytes(D, keep2, hmask2), x0h2, pkt_len2);
     if (valid2 && c == 0) sizes[slot0 + (uint32_t)i2] = pkt_len2;
-    GSO_STAMP(4);
     return;
   }
 
@@ -796,7 +919,6 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
     }
   }
   if (r == 0) sizes[slot] = pkt_len;
-  GSO_STAMP(4);
 }
 
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs, uint8_t* out,

@@ -14,8 +14,8 @@
 // k+1's kernel and batch k+2's H2D overlap.  The output of a batch is packed:
 // read r's segments sit at base_r + i*pitch_r, where the host derives a pitch
 // that holds any segment the kernel may produce from the 10-byte virtio header
-// (gsoSize + the kernel's 240-byte header limit, or the whole packet for
-// GSO_NONE), so the D2H moves about the produced bytes instead of
+// (min(read, header bound + gsoSize), or the whole packet for GSO_NONE), so
+// the D2H moves about the produced bytes instead of
 // max_segs fixed-size slots per read.  The handleVirtioRead room checks use
 // the caller's buffer room (seg_room), exactly as with bufs[i][offset:].
 #include <hip/hip_runtime.h>
@@ -43,6 +43,7 @@ struct Slot {
   size_t used_in = 0, used_out = 0;
   int reserved = -1;
   size_t reserved_max = 0;
+  size_t carry = 0;  // committed read (bytes at h_in + used_in) whose output region did not fit: moved by submit
   // pinned host
   uint8_t* h_in = nullptr;
   wgcs_gso_job* h_jobs = nullptr;
@@ -108,6 +109,7 @@ int open_slot(wgcs_stager* st, uint32_t idx) {
   s.n_reads = 0;
   s.used_in = s.used_out = 0;
   s.reserved = -1;
+  s.carry = 0;
   st->open = idx;
   return WGCS_OK;
 }
@@ -115,6 +117,7 @@ int open_slot(wgcs_stager* st, uint32_t idx) {
 int stage(wgcs_stager* st, size_t max_n, uint8_t** dst, int* read_idx) {
   Slot& s = st->slots[st->open];
   if (s.reserved >= 0) return set_err(st->ctx, WGCS_ERR_INVALID_ARG, "stager: commit the open reservation first");
+  if (s.carry) return set_err(st->ctx, WGCS_ERR_BATCH_FULL, "stager: a committed read waits for submit");
   if (max_n > 0x7FFFFFF0u) return set_err(st->ctx, WGCS_ERR_INVALID_ARG, "read too large");
   if (s.n_reads >= st->max_reads || s.used_in + align16(max_n) > st->max_in)
     return set_err(st->ctx, WGCS_ERR_BATCH_FULL, "stager: open batch is full");
@@ -126,7 +129,7 @@ int stage(wgcs_stager* st, size_t max_n, uint8_t** dst, int* read_idx) {
 int finish(wgcs_stager* st, size_t n) {
   Slot& s = st->slots[st->open];
   uint32_t pitch, segs;
-  gso_out_layout(s.h_in + s.used_in, n, st->max_segs, &pitch, &segs);
+  gso_out_layout(s.h_in + s.used_in, n, 0, st->max_segs, &pitch, &segs);
   const size_t region = (size_t)pitch * segs;
   if (s.used_out + region > st->max_out)
     return set_err(st->ctx, WGCS_ERR_BATCH_FULL, "stager: output region of the open batch is full");
@@ -257,7 +260,14 @@ int wgcs_stager_commit(wgcs_stager* st, int read_idx, size_t n) {
     return set_err(st->ctx, WGCS_ERR_INVALID_ARG, "stager: commit without a matching reservation");
   s.reserved = -1;
   if (n == 0) return WGCS_OK;  // nothing read: the reservation is dropped
-  return finish(st, n);
+  const int rc = finish(st, n);
+  if (rc == WGCS_ERR_BATCH_FULL) {
+    if (s.n_reads == 0) return set_err(st->ctx, WGCS_ERR_INVALID_ARG, "stager: one read's output exceeds max_out");
+    // the bytes read(2) put into the slot stay: submit() queues this batch
+    // without them and carries them into the next one (no read is lost)
+    s.carry = n;
+  }
+  return rc;
 }
 
 int wgcs_stager_submit(wgcs_stager* st, uint64_t* batch) {
@@ -288,7 +298,15 @@ int wgcs_stager_submit(wgcs_stager* st, uint64_t* batch) {
   if (e != hipSuccess) return hip_fail(st->ctx, e, "stager submit");
   s.state = 2;
   *batch = s.id;
-  return open_slot(st, (st->open + 1) % st->depth);
+  const size_t carry = s.carry;
+  const uint8_t* carry_src = s.h_in + s.used_in;  // not part of this batch's H2D
+  int rc = open_slot(st, (st->open + 1) % st->depth);
+  if (rc || !carry) return rc;
+  Slot& t = st->slots[st->open];
+  memcpy(t.h_in, carry_src, carry);
+  rc = finish(st, carry);  // read 0 of the new batch
+  return rc == WGCS_ERR_BATCH_FULL ? set_err(st->ctx, WGCS_ERR_INVALID_ARG, "stager: one read's output exceeds max_out")
+                                   : rc;
 }
 
 int wgcs_stager_wait(wgcs_stager* st, uint64_t batch) {
@@ -325,23 +343,26 @@ int wgcs_stager_copy_out(wgcs_stager* st, uint64_t batch, int read_idx, uint8_t*
   if (!st || !bufs || !buf_lens || !sizes || !n_out || offset < 0) return WGCS_ERR_INVALID_ARG;
   if ((uint32_t)nbufs != st->max_segs)
     return set_err(st->ctx, WGCS_ERR_INVALID_ARG, "copy_out: nbufs must equal the stager's max_segs");
-  int status, n;
-  const int32_t* sz;
-  const uint8_t* seg;
-  int rc = wgcs_stager_result(st, batch, read_idx, &status, &n, &sz, &seg);
-  if (rc) return rc;
   *n_out = 0;
+  std::lock_guard<std::mutex> g(st->mu);  // the slot cannot be recycled while its results are copied
+  Slot* s = st->find(batch);
+  if (!s || s->state == 1 || hipEventQuery(s->done) != hipSuccess) return WGCS_ERR_NOT_READY;
+  if (read_idx < 0 || (uint32_t)read_idx >= s->n_reads) return WGCS_ERR_INVALID_ARG;
+  const int32_t* cnt = s->h_meta + (size_t)st->max_reads * st->max_segs;
+  const int n = cnt[read_idx];
+  const int status = cnt[st->max_reads + read_idx];
   if (status != 0 && status != WGCS_ERR_TOO_MANY_SEGMENTS) return status;
+  const int32_t* sz = s->h_meta + (size_t)read_idx * st->max_segs;
+  const uint8_t* seg = s->h_out + s->h_pos[read_idx].base;
+  const uint32_t pitch = s->h_pos[read_idx].pitch;
+  const uint8_t* vb = s->h_in + s->h_jobs[read_idx].off;
+  const size_t vlen = s->h_jobs[read_idx].len;
   const int written = status == WGCS_ERR_TOO_MANY_SEGMENTS ? nbufs : n;
-  uint32_t pitch;
-  {
-    std::lock_guard<std::mutex> g(st->mu);
-    pitch = st->find(batch)->h_pos[read_idx].pitch;
-  }
   for (int i = 0; i < written; ++i) {
     sizes[i] = sz[i];
-    if (buf_lens[i] < (size_t)offset + (size_t)sz[i]) {  // the Go code would panic on this slice
-      *n_out = i;
+    const bool last = status == 0 && i == written - 1;
+    if (buf_lens[i] < (size_t)offset + gso_split_need(vb, vlen, 0, (size_t)sz[i], last)) {
+      *n_out = i;  // the Go code would panic on this slice
       return WGCS_ERR_OUT_OF_RANGE;
     }
     memcpy(bufs[i] + offset, seg + (size_t)i * pitch, (size_t)sz[i]);

@@ -14,7 +14,6 @@ struct LaunchTuning {
   int unroll = 4;          // 16-byte loads in flight per lane per iteration
   int nt = 1;              // non-temporal (streaming) loads: each byte is read once
   int align = 16;          // chunk grid origin: packet start rounded down to this many bytes
-  int flat = 0;            // 16-lane rows only: stream back-to-back packet groups as one run (flat_group)
 };
 
 hipError_t launch_checksum_batch(int mode, unsigned flags, uint8_t* arena, const wgcs_pkt* pkts,
@@ -31,23 +30,54 @@ struct GsoOutPos {
   uint32_t pad;
 };
 // Packed-layout pitch and segment bound of one job ([10-byte virtio header |
-// packet], n bytes) from its virtio header: every segment gso_rows_kernel can
-// write for it fits in `pitch` (headers above 240 bytes fail OUT_OF_RANGE),
-// and it writes at most `segs` of them; 0/0 when it writes none.
-inline void gso_out_layout(const uint8_t* vb, size_t n, uint32_t max_segs, uint32_t* pitch, uint32_t* segs) {
+// packet], n bytes) from its virtio header and job flags: every segment
+// gso_rows_kernel can write for it fits in `pitch` (a segment is at most
+// min(len, hdrLen + gsoSize) bytes; hdrLen is the caller's for RAW jobs and at
+// most csumStart + 60 after handleVirtioRead's recompute), and it writes at
+// most `segs` of them; 0/0 when it writes none.
+inline void gso_out_layout(const uint8_t* vb, size_t n, uint32_t jflags, uint32_t max_segs, uint32_t* pitch,
+                           uint32_t* segs) {
   *pitch = 0;
   *segs = 0;
   if (n <= 10) return;  // short buffer / empty packet: nothing written
   const size_t plen = n - 10;
-  const uint32_t gso = (uint32_t)vb[4] | ((uint32_t)vb[5] << 8);
-  if (vb[1] == 0) {  // GSO_NONE: the packet itself
+  const size_t gso = (size_t)vb[4] | ((size_t)vb[5] << 8);
+  const bool raw = (jflags & WGCS_GSO_JOB_RAW) != 0;
+  if (!raw && vb[1] == 0) {  // GSO_NONE: the packet itself
     *pitch = (uint32_t)((plen + 15) & ~(size_t)15);
     *segs = 1;
     return;
   }
-  *pitch = (240u + gso + 15u) & ~15u;
+  const size_t cs = (size_t)vb[6] | ((size_t)vb[7] << 8);
+  const size_t hdr = raw ? ((size_t)vb[2] | ((size_t)vb[3] << 8)) : cs + 60;
+  size_t seg = hdr + gso < plen ? hdr + gso : plen;
+  if (seg < 16) seg = 16;
+  *pitch = (uint32_t)((seg + 15) & ~(size_t)15);
   const size_t nseg = gso ? (plen + gso - 1) / gso + 1 : (size_t)max_segs;
   *segs = (uint32_t)(nseg < max_segs ? nseg : max_segs);
+}
+
+// Bytes of bufs[i][offset:] that segment i (pkt_len bytes, `last` or not) of
+// the job vb ([10-byte virtio header | packet], n bytes) writes: the packet
+// plus gsoSplit's fixed-position header writes (gro.go:1419-1488 -- IPv4
+// [2:12) or IPv6 [4:6), seq / UDP length at csumStart+4, the TCP flags byte on
+// non-last segments, the checksum field; u16 positions).  A shorter Go slice
+// panics, so the host entry points report OUT_OF_RANGE there.  GSO_NONE
+// (handleVirtioRead semantics) writes the packet only.
+inline size_t gso_split_need(const uint8_t* vb, size_t n, uint32_t jflags, size_t pkt_len, bool last) {
+  if (n < 10) return pkt_len;
+  const bool raw = (jflags & WGCS_GSO_JOB_RAW) != 0;
+  const uint8_t t = vb[1];
+  if (!raw && t == 0) return pkt_len;
+  const bool v4 = raw ? (jflags & WGCS_GSO_JOB_V6) == 0 : (n > 10 && (vb[10] >> 4) == 4);
+  const bool tcp = t == 1 || t == 4;
+  const uint16_t cs = (uint16_t)(vb[6] | (vb[7] << 8)), co = (uint16_t)(vb[8] | (vb[9] << 8));
+  size_t need = pkt_len > (size_t)(v4 ? 12 : 6) ? pkt_len : (size_t)(v4 ? 12 : 6);
+  size_t f = (size_t)(uint16_t)(cs + 4) + (tcp ? 4 : 2);
+  if (f > need) need = f;
+  if (tcp && !last && (f = (size_t)(uint16_t)(cs + 13) + 1) > need) need = f;
+  if ((f = (size_t)(uint16_t)(cs + co) + 2) > need) need = f;
+  return need;
 }
 
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs,
@@ -70,7 +100,9 @@ struct GroSeg {
   uint32_t src_off, len;  // stage offset / length of one payload piece
   uint32_t dst_off, pad;  // output offset of the piece (host-computed: pieces copy in parallel)
 };
-enum : uint8_t { GRO_KIND_V6 = 1, GRO_KIND_UDP = 2, GRO_KIND_PSH = 4 };
+// RAW: the coalesced bytes only (head packet header + PSH, no apply*, no virtio
+// header) -- handleGRO stopped at an invalid offset before applyTCPCoalesce.
+enum : uint8_t { GRO_KIND_V6 = 1, GRO_KIND_UDP = 2, GRO_KIND_PSH = 4, GRO_KIND_RAW = 8 };
 
 hipError_t launch_gro_coalesce(const uint8_t* stage, const GroItem* items, uint32_t n_items, const GroSeg* segs,
                                uint32_t n_segs, uint8_t* out, hipStream_t s);

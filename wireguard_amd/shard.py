@@ -43,14 +43,7 @@ def make_global_shard(n_total: int, rank: int, world: int, frame_len: int = 1500
     arena = np.concatenate(parts + [np.zeros(64, np.uint8)])
     k = np.concatenate(kparts) if kparts else np.zeros(0, np.int64)
     m = hi - lo
-    pkts = np.zeros(m, dtype=synth.PKT_DTYPE)
-    pkts["off"] = np.arange(m, dtype=np.uint64) * np.uint64(frame_len)
-    pkts["len"] = frame_len
-    v6 = (k == synth.KIND_TCP6) | (k == synth.KIND_UDP6)
-    udp = (k == synth.KIND_UDP4) | (k == synth.KIND_UDP6)
-    pkts["csum_start"] = np.where(v6, 40, 20)
-    pkts["csum_offset"] = np.where(udp, 6, 16)
-    pkts["flags"] = (v6 * synth.FLAG_V6) | (udp * synth.FLAG_UDP)
+    pkts = synth.describe(k, frame_len, np.arange(m, dtype=np.uint64) * np.uint64(frame_len))
     return arena, pkts, k, lo, hi
 
 

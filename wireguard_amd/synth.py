@@ -16,11 +16,9 @@ import numpy as np
 
 SEED = 20261015
 
-PKT_DTYPE = np.dtype(
-    [("off", "<u8"), ("len", "<u4"), ("csum_start", "<u2"), ("csum_offset", "u1"), ("flags", "u1")]
-)
+from .tun import PKT_DTYPE, pkt_off, set_pkt_off  # noqa: E402,F401  (wgcs_pkt, include/wgcsum.h)
+
 FLAG_V6 = 0x01
-FLAG_UDP = 0x02
 KIND_TCP4, KIND_UDP4, KIND_TCP6, KIND_UDP6 = 0, 1, 2, 3
 
 
@@ -135,15 +133,23 @@ def make_batch(n: int, frame_len: int = 1500, kinds="tcp4", seed: int = SEED,
     for lo in range(0, n, chunk):
         hi = min(n, lo + chunk)
         view[lo:hi, :frame_len] = build_frames(k[lo:hi], frame_len, rng, valid=valid)
-    pkts = np.zeros(n, dtype=PKT_DTYPE)
-    pkts["off"] = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    pkts = describe(k, frame_len, np.arange(n, dtype=np.uint64) * np.uint64(stride))
+    return arena, pkts, k
+
+
+def describe(kinds: np.ndarray, frame_len, offsets) -> np.ndarray:
+    """wgcs_pkt descriptors of frames of the given kinds at the given arena offsets."""
+    k = np.asarray(kinds)
+    pkts = np.zeros(len(k), dtype=PKT_DTYPE)
+    set_pkt_off(pkts, offsets)
     pkts["len"] = frame_len
     v6 = (k == KIND_TCP6) | (k == KIND_UDP6)
     udp = (k == KIND_UDP4) | (k == KIND_UDP6)
     pkts["csum_start"] = np.where(v6, 40, 20)
     pkts["csum_offset"] = np.where(udp, 6, 16)
-    pkts["flags"] = (v6 * FLAG_V6) | (udp * FLAG_UDP)
-    return arena, pkts, k
+    pkts["proto"] = np.where(udp, 17, 6)
+    pkts["flags"] = v6 * FLAG_V6
+    return pkts
 
 
 def make_super_packet(total_len: int = 65535, gso_size: int = 1460, seed: int = SEED,

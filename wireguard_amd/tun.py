@@ -21,12 +21,28 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import (MODE_FOLD, MODE_L4_FILL, MODE_VALIDATE, MODE_PARTIAL, MODE_IP4HDR, F_INPLACE, PKT_V6, PKT_UDP,
+from ._lib import (MODE_FOLD, MODE_L4_FILL, MODE_VALIDATE, MODE_PARTIAL, MODE_IP4HDR, F_INPLACE, PKT_V6,
                    VirtioHdr, WgcsError)
 
+# wgcs_pkt (include/wgcsum.h, ABI 2): 48-bit arena offset split in two fields,
+# pseudo-header protocol, flags (PKT_V6), length, csum_start, u16 csum_offset
 PKT_DTYPE = np.dtype(
-    [("off", "<u8"), ("len", "<u4"), ("csum_start", "<u2"), ("csum_offset", "u1"), ("flags", "u1")]
+    [("off_lo", "<u4"), ("off_hi", "<u2"), ("proto", "u1"), ("flags", "u1"), ("len", "<u4"),
+     ("csum_start", "<u2"), ("csum_offset", "<u2")]
 )
+IPPROTO_TCP, IPPROTO_UDP = 6, 17
+
+
+def set_pkt_off(pkts: np.ndarray, off) -> None:
+    """Store arena offsets (< 2**48) into a PKT_DTYPE array."""
+    off = np.asarray(off, dtype=np.uint64)
+    pkts["off_lo"] = (off & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    pkts["off_hi"] = (off >> np.uint64(32)).astype(np.uint16)
+
+
+def pkt_off(pkts: np.ndarray) -> np.ndarray:
+    """Arena offsets of a PKT_DTYPE array (uint64)."""
+    return pkts["off_lo"].astype(np.uint64) | (pkts["off_hi"].astype(np.uint64) << np.uint64(32))
 GSO_JOB_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("pad", "<u4")])
 
 VIRTIO_NET_HDR_LEN = 10
@@ -38,7 +54,8 @@ VIRTIO_NET_HDR_GSO_UDP_L4 = 5
 
 __all__ = [
     "Device", "Stager", "PKT_DTYPE", "GSO_JOB_DTYPE", "MODE_FOLD", "MODE_L4_FILL", "MODE_VALIDATE", "MODE_PARTIAL",
-    "MODE_IP4HDR", "F_INPLACE", "PKT_V6", "PKT_UDP", "VirtioHdr", "WgcsError",
+    "MODE_IP4HDR", "F_INPLACE", "PKT_V6", "IPPROTO_TCP", "IPPROTO_UDP", "VirtioHdr", "WgcsError", "set_pkt_off",
+    "pkt_off",
 ]
 
 
