@@ -32,10 +32,17 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# Host completion wait: spin on the HIP completion signal instead of sleeping
+# on the interrupt after the runtime's default 10 us, as a latency-bound
+# packet datapath would (busy-poll).  Host-side only: the GPU work is the same.
+# Must be set before the HIP runtime initialises (torch import).
+os.environ.setdefault("ROC_ACTIVE_WAIT_TIMEOUT", "100000")
+
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 CONFIGS = {
     # name: (packets, frame_len, kinds, BASELINE.json configs index, scaling)
+    "cfg1": (1024, 1500, "udp4", 0, "weak"),  # the reference's CPU plumbing case; GPU leg as context
     "cfg2": (65536, 1500, "tcp4", 1, "weak"),
     "cfg3": (65536, 9000, "tcp4", 2, "weak"),
     "cfg5": (1048576, 1500, "mixed", 4, "strong"),  # global batch, split across the ranks
@@ -49,9 +56,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS) + ["cfg4", "gro", "udp_split", "udp_coalesce"])
+    ap.add_argument("--config", default="cfg2",
+                    choices=sorted(CONFIGS) + ["cfg4", "gro", "gro_staged", "udp_split", "udp_coalesce"])
     ap.add_argument("--mode", default="validate", choices=["validate", "fill"])
     ap.add_argument("--rotate", type=int, default=4, help="distinct batch copies (defeat the 256 MiB MALL)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="launch streams, consecutive batches round-robin (0: 2, or 1 for the launch-bound cfg1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-event-timing", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end measurement")
@@ -61,6 +71,8 @@ def parse():
 
 def main():
     args = parse()
+    if args.streams <= 0:
+        args.streams = 1 if args.config == "cfg1" else 2
     import torch  # before wireguard_amd: one HIP runtime per process
 
     from wireguard_amd import shard, synth, traffic
@@ -98,6 +110,10 @@ def main():
         from wireguard_amd import gro_bench
 
         return gro_bench.run(args, torch, dev, dist, rank, world, local, barrier)
+    if args.config == "gro_staged":
+        from wireguard_amd import gro_bench
+
+        return gro_bench.run_staged(args, torch, dev, dist, rank, world, local, barrier)
     if args.config in ("udp_split", "udp_coalesce"):
         from wireguard_amd import udp_bench
 
@@ -111,16 +127,22 @@ def main():
         arena_np, pkts_np, _ = synth.make_batch(n_cfg, flen, kinds=kinds, seed=synth.SEED + rank)
     n = len(pkts_np)
     bytes_per_step = int(pkts_np["len"].astype(np.int64).sum())
-    stream = torch.cuda.Stream()  # dedicated stream: kernel launches and events share it
+    # Consecutive steps are independent batches (their own rotated arena and
+    # output), launched round-robin over S streams: step k+1's kernel streams
+    # while step k's drains and pays its end-of-kernel L2 writeback, which a
+    # single stream serialises (~1.7 us per boundary, MI355X_MICROARCH.md).
+    S = max(1, args.streams)
+    streams = [torch.cuda.Stream() for _ in range(S)]
     R = args.rotate if bytes_per_step * args.rotate > (300 << 20) else max(args.rotate, (400 << 20) // bytes_per_step)
+    R = max(R, 2 * S)
     arenas = [torch.from_numpy(arena_np).to("cuda") for _ in range(R)]
     pkts = torch.from_numpy(pkts_np.view(np.uint8)).to("cuda")
     outs = [torch.empty(n * 2, dtype=torch.uint8, device="cuda") for _ in range(R)]
     torch.cuda.synchronize()
 
-    def step(k):
+    def step(k, ns=S):
         i = k % R
-        dev.checksum_batch(mode, arenas[i], pkts, n, outs[i], stream=stream)
+        dev.checksum_batch(mode, arenas[i], pkts, n, outs[i], stream=streams[k % ns])
 
     for k in range(args.warmup):
         step(k)
@@ -135,27 +157,40 @@ def main():
             want = (a[np.arange(n), cs].astype(np.uint16) << 8) | a[np.arange(n), cs + 1]
             assert np.array_equal(got, want), "L4_FILL mismatch vs stored checksums"
 
-    # HIP events on the launch stream bracket the timed region (one pair: an
-    # event between launches would add a ~10 us gap per step); launches are
-    # back-to-back on one stream, so elapsed / steps = the average launch
-    # duration rocprofv3 reports for the kernel (profiles/).
+    # HIP events bracket the timed region on the launch streams: e0 on stream 0
+    # (the others wait on it), every other stream joins stream 0 before e1, so
+    # (e1 - e0) / steps is the GPU time per launch over the timed region (an
+    # event between launches would add a gap per step).
     use_events = not args.no_event_timing
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    if use_events:
-        e0.record(stream)
-    for k in range(args.steps):
-        step(args.warmup + k)
-    if use_events:
-        e1.record(stream)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = e0.elapsed_time(e1) / args.steps if use_events else None
+    joins = [torch.cuda.Event() for _ in streams[1:]]
+
+    def timed(K, k0, ns):
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if use_events:
+            e0.record(streams[0])
+            for st in streams[1:ns]:
+                st.wait_event(e0)
+        for k in range(K):
+            step(k0 + k, ns)
+        for j, st in zip(joins, streams[1:ns]):
+            j.record(st)
+            streams[0].wait_event(j)
+        if use_events:
+            e1.record(streams[0])
+        torch.cuda.synchronize()
+        barrier()
+        el = time.perf_counter() - t0
+        return el, (e0.elapsed_time(e1) / K if use_events else None)
+
+    elapsed, kern_ms = timed(args.steps, args.warmup, S)
     elapsed = shard.max_over_ranks(elapsed, dist, device=red_dev)
+    iso_ms = None
+    if use_events and S > 1:  # reference: the same launches one at a time on one stream (untimed for `value`)
+        _, iso_ms = timed(max(args.steps, 20), args.warmup + args.steps, 1)
 
     total_bytes = bytes_per_step * args.steps * world  # every rank processed bytes_per_step per step
     if scaling == "strong":
@@ -184,6 +219,7 @@ def main():
             "global_batch_bytes": bytes_per_step * world if scaling == "weak" else n_cfg * flen,
             "mode": args.mode,
             "rotated_copies": R,
+            "streams": S,
             "parallelism": f"shard{world} (no collective)",
         },
     }
@@ -198,12 +234,21 @@ def main():
             "traffic": traffic.per_launch(kname, bytes_per_step),
             "kernel": kname,
             "kernel_ms": round(kern_ms, 5),
+            "kernel_ms_is": ("GPU time per launch over the timed region (HIP events on the launch streams)"
+                             + (f"; {S} streams, consecutive launches overlap" if S > 1 else "")),
             "algorithmic_bytes_per_launch": bytes_per_step,
             "algorithmic_bytes_per_unit": flen,
             "units_per_launch": n,
         }
-    if rank == 0 and world == 1 and not args.no_e2e:
-        result["end_to_end"] = end_to_end(torch, dev, arena_np, pkts_np, mode, stream)
+        if iso_ms is not None:
+            result["roofline"]["kernel_ms_one_stream"] = round(iso_ms, 5)
+            result["roofline"]["frac_one_stream"] = round(bytes_per_step / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    if not args.no_e2e:  # every rank moves its own shard over its own PCIe link; rank 0 reports the aggregate
+        e2e = end_to_end(torch, dev, arena_np, pkts_np, mode, barrier, dist, red_dev, world)
+        if rank == 0:
+            result["end_to_end"] = e2e
+    if rank == 0 and world == 1 and args.config == "cfg1" and not args.no_e2e:
+        result["host_call"] = host_call(dev, arena_np, pkts_np, mode)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(arena_np, pkts_np, mode, args.cpu_seconds)
     if rank == 0:
@@ -218,6 +263,7 @@ def _tune_tag():
     LaunchTuning: 32 lanes per packet, 4 loads in flight per lane) or the
     WGCS_LANES_PER_PKT / WGCS_UNROLL overrides api.cpp reads."""
     g = int(os.environ.get("WGCS_LANES_PER_PKT", "32"))
+    x = "" if os.environ.get("WGCS_XCD", "1") != "0" else ",noxcd"
     u = int(os.environ.get("WGCS_UNROLL", "4"))
     if g == 32:
         u = 6 if u >= 6 else (4 if u >= 4 else 3)
@@ -225,33 +271,80 @@ def _tune_tag():
         u = 4 if u >= 4 else 2
     else:
         g, u = 16, (8 if u >= 8 else (6 if u >= 6 else 4))
-    return f"{g},{u}"
+    return f"{g},{u}{x}"
 
 
-def end_to_end(torch, dev, arena_np, pkts_np, mode, stream, iters=20):
-    """Host -> device -> host rate: pinned H2D of the batch, the kernel, D2H of
-    the per-packet results (the path starts and ends in host memory, tun/tun.go:490,:688)."""
+def end_to_end(torch, dev, arena_np, pkts_np, mode, barrier, dist, red_dev, world, iters=10, chunks=8):
+    """Host -> device -> host rate (the path starts and ends in host memory,
+    tun/tun.go:490, :688): pinned H2D of the batch, the kernel, D2H of the
+    per-packet results, double-buffered -- the batch goes in `chunks` pieces
+    alternating over two streams, so chunk k+1's H2D overlaps chunk k's kernel
+    and D2H.  Every rank runs it at once on its own GPU and PCIe link; the
+    aggregate is all ranks' bytes over the slowest rank's time."""
+    from wireguard_amd import tun
+
     n = len(pkts_np)
     nbytes = int(pkts_np["len"].astype(np.int64).sum())
+    out_b = 1 if mode == tun.MODE_VALIDATE else 2
     h_arena = torch.from_numpy(arena_np).pin_memory()
     h_out = torch.empty(n * 2, dtype=torch.uint8).pin_memory()
     d_arena = torch.empty(len(arena_np), dtype=torch.uint8, device="cuda")
-    d_pkts = torch.from_numpy(pkts_np.view(np.uint8)).to("cuda")
     d_out = torch.empty(n * 2, dtype=torch.uint8, device="cuda")
-    out_b = n if mode == 2 else 2 * n
-    with torch.cuda.stream(stream):
-        for it in range(iters + 3):
-            if it == 3:
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-            d_arena.copy_(h_arena, non_blocking=True)
-            dev.checksum_batch(mode, d_arena, d_pkts, n, d_out, stream=stream)
-            h_out[:out_b].copy_(d_out[:out_b], non_blocking=True)
-        torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / iters
-    return {"value": round(nbytes / dt / 2**30, 2), "unit": "GiB/s", "ms_per_batch": round(dt * 1e3, 4),
-            "what": "pinned H2D of the batch + kernel + D2H of the per-packet results, serialized on one "
-                    "stream (PCIe Gen5 x16 bound)"}
+    offs = tun.pkt_off(pkts_np)
+    # chunk c: packets [lo, hi), arena bytes [offs[lo], end of packet hi-1), descriptors rebased to the chunk
+    bounds = [n * c // chunks for c in range(chunks + 1)]
+    parts = []
+    for c in range(chunks):
+        lo, hi = bounds[c], bounds[c + 1]
+        if lo == hi:
+            continue
+        a0 = int(offs[lo])
+        a1 = len(arena_np) if hi == n else int(offs[hi])
+        sub = pkts_np[lo:hi].copy()
+        tun.set_pkt_off(sub, offs[lo:hi] - np.uint64(a0))
+        parts.append((lo, hi, a0, a1, torch.from_numpy(sub.view(np.uint8)).to("cuda")))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+
+    def one_batch():
+        for k, (lo, hi, a0, a1, d_p) in enumerate(parts):
+            s = streams[k & 1]
+            with torch.cuda.stream(s):
+                d_arena[a0:a1].copy_(h_arena[a0:a1], non_blocking=True)
+                dev.checksum_batch(mode, d_arena[a0:], d_p, hi - lo, d_out[lo * out_b:], stream=s)
+                h_out[lo * out_b: hi * out_b].copy_(d_out[lo * out_b: hi * out_b], non_blocking=True)
+
+    for _ in range(2):
+        one_batch()
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        one_batch()
+    torch.cuda.synchronize()
+    barrier()
+    from wireguard_amd import shard
+
+    dt = shard.max_over_ranks((time.perf_counter() - t0) / iters, dist, device=red_dev)
+    return {"value": round(world * nbytes / dt / 2**30, 2), "unit": "GiB/s", "ms_per_batch": round(dt * 1e3, 4),
+            "n_gpus": world,
+            "what": f"pinned H2D of the batch + kernel + D2H of the per-packet results, {len(parts)} chunks "
+                    "double-buffered over two streams, every rank at once (aggregate; PCIe bound)"}
+
+
+def host_call(dev, arena_np, pkts_np, mode, reps=50):
+    """The reference-shaped host entry (wgcs_checksum_batch_host: host arena
+    in, results out, one round trip) on the whole batch, median per call."""
+    arena = arena_np.copy()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        dev.checksum_batch_host(mode, arena, pkts_np)
+        ts.append(time.perf_counter() - t0)
+    med = float(np.median(ts))
+    nbytes = int(pkts_np["len"].astype(np.int64).sum())
+    return {"call": "wgcs_checksum_batch_host on the whole batch (host buffers, one PCIe round trip)",
+            "median_us": round(med * 1e6, 1), "GiB_per_s": round(nbytes / med / 2**30, 3)}
 
 
 def _time_oracle(oracle, mode, arena_np, pkts_np, threads, seconds):
@@ -267,17 +360,26 @@ def _time_oracle(oracle, mode, arena_np, pkts_np, threads, seconds):
 
 
 def cpu_baseline(arena_np, pkts_np, mode, seconds):
-    """The oracle (C restatement of tun/checksum.go) on the same batch: the
-    headline leg on 1 thread for `seconds`, plus an all-host-cores leg
-    (pthreads over packet ranges) for a quarter of that."""
+    """The oracle (C restatement of tun/checksum.go) on the same batch: one
+    thread for `seconds`, plus an all-host-cores leg for a quarter of that --
+    pthreads over packet ranges of the one batch, or, for batches under 64 MB
+    (cfg1: a pass is too short to split), every thread running whole passes
+    over its own copy."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # cpu_baseline leg: allowed use of the oracle
 
     nbytes = int(pkts_np["len"].astype(np.int64).sum())
     reps, dt = _time_oracle(oracle, mode, arena_np, pkts_np, 1, seconds)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
-    reps_mt, dt_mt = _time_oracle(oracle, mode, arena_np, pkts_np, threads, max(seconds / 4, 0.5))
+    threads = oracle.host_threads()
+    mt_seconds = max(seconds / 4, 0.5)
+    if arena_np.nbytes < (64 << 20):
+        rate, passes = oracle.checksum_bench_mt(mode, arena_np, pkts_np, threads, mt_seconds)
+        mt = {"value": round(nbytes * rate / 2**30, 3),
+              "sample": f"{passes} whole-batch passes on {threads} pthreads, each on its own copy, {mt_seconds:.1f} s"}
+    else:
+        reps_mt, dt_mt = _time_oracle(oracle, mode, arena_np, pkts_np, threads, mt_seconds)
+        mt = {"value": round(nbytes * reps_mt / dt_mt / 2**30, 3),
+              "sample": f"{reps_mt} passes, {dt_mt:.1f} s, {threads} pthreads over packet ranges"}
     return {
         "value": round(nbytes * reps / dt / 2**30, 3),
         "unit": "GiB/s",
@@ -285,8 +387,7 @@ def cpu_baseline(arena_np, pkts_np, mode, seconds):
         "kind": "port",
         "sample": f"{reps} passes over the same {len(pkts_np)}-frame batch ({nbytes/1e6:.1f} MB), "
                   f"{dt:.1f} s, C -O3 restatement of tun/checksum.go + checksumValid, 1 thread",
-        "all_cores": {"value": round(nbytes * reps_mt / dt_mt / 2**30, 3), "unit": "GiB/s", "cores": threads,
-                      "sample": f"{reps_mt} passes, {dt_mt:.1f} s, {threads} pthreads over packet ranges"},
+        "all_cores": dict(mt, unit="GiB/s", cores=threads, host_nproc=os.cpu_count()),
     }
 
 

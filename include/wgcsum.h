@@ -28,6 +28,8 @@
  *   wgcs_split_messages_batch device-resident batch of splitMessages calls (one per recvmmsg)
  *   wgcs_coalesce_messages    coalesceMessages(msgs, bufs, ep, addr)  conn/bind.go:599-662
  *   wgcs_coalesce_messages_batch  device-resident batch of coalesceMessages calls (one per Send)
+ *   wgcs_stager_*             Tun.Read batch staging              tun/tun.go:477-508
+ *   wgcs_wstager_*            Tun.Write batch staging             tun/tun.go:654-700
  * Status codes map 1:1 onto the reference's Go errors (see WGCS_ERR_*).
  */
 #ifndef WGCSUM_H
@@ -210,7 +212,10 @@ int wgcs_stager_push(wgcs_stager *st, const uint8_t *read_buf, size_t n, int *re
 int wgcs_stager_push_many(wgcs_stager *st, const uint8_t *const *read_bufs, const size_t *ns, int count,
                           int *first_idx, int *pushed);
 /* zero-copy form: reserve room for up to max_n bytes (read(2) goes straight
- * into *dst), then commit the byte count read (0 drops the reservation) */
+ * into *dst), then commit the byte count read (0 drops the reservation).  If
+ * the read's output region does not fit the open batch, commit returns
+ * WGCS_ERR_BATCH_FULL and keeps the bytes: the next wgcs_stager_submit queues
+ * the batch without them and carries them in as read 0 of the new batch. */
 int wgcs_stager_reserve(wgcs_stager *st, size_t max_n, uint8_t **dst, int *read_idx);
 int wgcs_stager_commit(wgcs_stager *st, int read_idx, size_t n);
 /* queue the open batch (no-op id for an empty batch) and open the next one */
@@ -223,6 +228,39 @@ int wgcs_stager_result(wgcs_stager *st, uint64_t batch, int read_idx, int *statu
  * leaves them (sizes[], n, ErrTooManySegments / slice-bound checks) */
 int wgcs_stager_copy_out(wgcs_stager *st, uint64_t batch, int read_idx, uint8_t *const *bufs,
                          const size_t *buf_lens, int nbufs, int *sizes, int offset, int *n_out);
+
+/* ---- Tun.Write batch staging (tun/tun.go:654-700) ----
+ * A ring of `depth` slots; a slot aggregates up to max_writes Tun.Write calls
+ * (<= max_pkts packets and <= max_bytes packet bytes in all).
+ * wgcs_wstager_push stages one Write call -- bufs[i][offset:lens[i]], the
+ * packets as device/receive.go:483 slices them, caps[i] = cap(bufs[i]) -- into
+ * pinned memory and plans its flows on the host assuming valid checksums.
+ * wgcs_wstager_submit queues, on the slot's own stream, one H2D of every staged
+ * packet, ONE checksumValid (VALIDATE) launch over every GRO candidate of every
+ * staged call, ONE coalesce launch over every merged super-packet, and the D2H
+ * of both.  wgcs_wstager_wait settles the slot: a call whose plan used a
+ * checksum found invalid is re-planned with the real bits (one more small
+ * round trip for that call only), so results are exactly handleGRO's
+ * (gro.go:1326-1367).  wgcs_wstager_result hands back, per call, what
+ * Tun.Write passes to write(2) (tun.go:687-698): to_write[k] = handleGRO's
+ * toWrite and pkts[k][0:pkt_lens[k]] = bufs[to_write[k]][offset-10:] after
+ * handleGRO (10-byte virtio header + packet) in pinned memory, valid until the
+ * slot is recycled; status WGCS_ERR_INVALID_OFFSET (gro.go:1336) writes
+ * nothing.  The caller's bufs are only read.  Ring discipline as the Read
+ * stager's: results stay readable until depth-1 more submits. */
+typedef struct wgcs_wstager wgcs_wstager;
+int wgcs_wstager_create(wgcs_ctx *ctx, uint32_t depth, uint32_t max_writes, uint32_t max_pkts, size_t max_bytes,
+                        wgcs_wstager **out);
+int wgcs_wstager_destroy(wgcs_wstager *ws);
+/* stage one Tun.Write(bufs, offset) call; *write_idx = its index in the open slot
+ * (WGCS_ERR_BATCH_FULL: submit first) */
+int wgcs_wstager_push(wgcs_wstager *ws, const uint8_t *const *bufs, const size_t *lens, const size_t *caps, int n,
+                      int offset, int can_udp_gro, int *write_idx);
+int wgcs_wstager_submit(wgcs_wstager *ws, uint64_t *batch);
+int wgcs_wstager_wait(wgcs_wstager *ws, uint64_t batch);
+/* to_write / pkts / pkt_lens hold at least n (the call's packet count) entries */
+int wgcs_wstager_result(wgcs_wstager *ws, uint64_t batch, int write_idx, int *status, int *n_write, int *to_write,
+                        const uint8_t **pkts, size_t *pkt_lens);
 
 /* ---- outer-UDP message batching (conn/bind.go, conn/gso.go) ----
  * The UDP side of the same batch loop: recvmmsg with UDP_GRO hands back up to

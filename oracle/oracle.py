@@ -67,6 +67,15 @@ def lib() -> C.CDLL:
         L.or_checksum_batch.restype = None
         L.or_checksum_batch_mt.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int]
         L.or_checksum_batch_mt.restype = None
+        L.or_gso_bench_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_double, C.POINTER(C.c_uint64)]
+        L.or_gso_bench_mt.restype = C.c_double
+        L.or_gro_bench_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_double, C.POINTER(C.c_uint64)]
+        L.or_gro_bench_mt.restype = C.c_double
+        L.or_checksum_bench_mt.argtypes = [C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32, C.c_int, C.c_double,
+                                           C.POINTER(C.c_uint64)]
+        L.or_checksum_bench_mt.restype = C.c_double
         _lib = L
     return _lib
 
@@ -114,6 +123,46 @@ def checksum_batch_mt(mode: int, arena: np.ndarray, pkts: np.ndarray, threads: i
     out = np.zeros(n, dtype=np.uint8 if mode == 2 else np.uint16)
     lib().or_checksum_batch_mt(mode, _ptr(arena), _ptr(pkts), n, _ptr(out), threads)
     return out
+
+
+def host_threads() -> int:
+    """Host threads for all-cores baselines: OMP_NUM_THREADS (16 on the GPU
+    box, its CPU share) capped by the process's CPU affinity."""
+    t = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    return max(1, min(t, len(os.sched_getaffinity(0))))
+
+
+def gso_bench_mt(reads: list, nbufs: int, buf_len: int, offset: int, threads: int, seconds: float):
+    """handleVirtioRead calls/s over `threads` pthreads (wg_oracle_bench.c)."""
+    arena = np.frombuffer(b"".join(reads), np.uint8)
+    lens = np.array([len(r) for r in reads], np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    calls = C.c_uint64(0)
+    rate = lib().or_gso_bench_mt(_ptr(arena), _ptr(offs), _ptr(lens), len(reads), nbufs, buf_len, offset, threads,
+                                 seconds, C.byref(calls))
+    return rate, calls.value
+
+
+def checksum_bench_mt(mode: int, arena: np.ndarray, pkts: np.ndarray, threads: int, seconds: float):
+    """Whole-batch passes/s summed over `threads` pthreads, each on its own
+    copy of the arena (wg_oracle_bench.c)."""
+    passes = C.c_uint64(0)
+    rate = lib().or_checksum_bench_mt(mode, _ptr(arena), arena.nbytes, _ptr(pkts), len(pkts), threads, seconds,
+                                      C.byref(passes))
+    return rate, passes.value
+
+
+def gro_bench_mt(pkts: list, offset: int, can_udp: bool, threads: int, seconds: float):
+    """handleGRO calls/s (one call = the whole batch) over `threads` pthreads."""
+    stride = max(len(p) for p in pkts)
+    a = np.zeros((len(pkts), stride), np.uint8)
+    for i, p in enumerate(pkts):
+        a[i, : len(p)] = np.frombuffer(p, np.uint8)
+    lens = np.array([len(p) for p in pkts], np.uint64)
+    calls = C.c_uint64(0)
+    rate = lib().or_gro_bench_mt(_ptr(a), _ptr(lens), stride, len(pkts), offset, int(can_udp), threads, seconds,
+                                 C.byref(calls))
+    return rate, calls.value
 
 
 def _bufs_ctypes(bufs):

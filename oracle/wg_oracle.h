@@ -109,6 +109,15 @@ void or_checksum_batch(int mode, uint8_t *arena, const or_pkt *pkts,
 void or_checksum_batch_mt(int mode, uint8_t *arena, const or_pkt *pkts,
                           uint32_t n, void *out, int threads);
 
+/* All-cores CPU baselines (wg_oracle_bench.c): calls per second summed over
+ * `threads` pthreads, each on private copies of the inputs, timing only the calls. */
+double or_gso_bench_mt(const uint8_t *arena, const size_t *offs, const size_t *lens, int n_jobs, int nbufs,
+                       int buf_len, int offset, int threads, double seconds, uint64_t *calls_out);
+double or_gro_bench_mt(const uint8_t *pkts, const size_t *pkt_lens, size_t stride, int n, int offset, int can_udp,
+                       int threads, double seconds, uint64_t *calls_out);
+double or_checksum_bench_mt(int mode, const uint8_t *arena, size_t arena_len, const or_pkt *pkts, uint32_t n,
+                            int threads, double seconds, uint64_t *passes_out);
+
 /* ---- outer-UDP message batching (conn/bind.go, conn/gso.go; wg_oracle_conn.c) ---- */
 /* one ipv6.Message: Buffers[0] (len/cap), N, OOB (len/cap), NN, Addr (opaque id) */
 typedef struct or_msg {

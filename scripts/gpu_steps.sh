@@ -9,7 +9,7 @@ ROOT=$(pwd)
 OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-TAG=${TAG:-r1}
+TAG=${TAG:-r2}
 step() {
   local name=$1 lim=$2; shift 2
   echo "== [$name] $(date +%T) $*"
@@ -39,10 +39,14 @@ for s in "$@"; do
     bench) step bench 400 python bench.py --steps 200 --warmup 20 ;;
     bench-noevt) step bench_noevt 300 python bench.py --steps 200 --warmup 20 --no-event-timing --cpu-seconds 0 ;;
     bench-fill) step bench_fill 300 python bench.py --steps 200 --warmup 20 --mode fill --cpu-seconds 0 ;;
-    bench-cfg3) step bench_cfg3 300 python bench.py --config cfg3 --steps 100 --warmup 10 --cpu-seconds 0 ;;
-    bench-cfg4) step bench_cfg4 300 python bench.py --config cfg4 --steps 100 --warmup 10 --cpu-seconds 0 ;;
+    bench-cfg3) step bench_cfg3 300 python bench.py --config cfg3 --steps 100 --warmup 10 --cpu-seconds 4 ;;
+    bench-cfg4) step bench_cfg4 300 python bench.py --config cfg4 --steps 100 --warmup 10 --cpu-seconds 4 ;;
+    bench-cfg4-1s) step bench_cfg4_1s 300 python bench.py --config cfg4 --steps 100 --warmup 10 --cpu-seconds 0 --streams 1 ;;
     bench-gro) step bench_gro 300 python bench.py --config gro --steps 200 --warmup 20 --cpu-seconds 3 ;;
-    bench-cfg5) step bench_cfg5 300 python bench.py --config cfg5 --steps 100 --warmup 10 --cpu-seconds 0 ;;
+    bench-gro-staged) step bench_gros 300 python bench.py --config gro_staged --steps 30 --warmup 5 --cpu-seconds 3 ;;
+    bench-cfg1) step bench_cfg1 300 python bench.py --config cfg1 --steps 200 --warmup 20 --cpu-seconds 5 ;;
+    bench-driver) step bench_drv 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench-cfg5) step bench_cfg5 300 python bench.py --config cfg5 --steps 100 --warmup 10 --cpu-seconds 4 ;;
     prof) (cd /tmp && step prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e) ;;
     pmc) (cd /tmp && step pmc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e --no-event-timing) ;;
     pmc-w) (cd /tmp && step pmcw 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$TAG" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --cpu-seconds 0 --no-e2e --no-event-timing) ;;

@@ -28,7 +28,7 @@ def flow(nseg, seg=1000, v6=False, udp=False, seed=0, last_flags=0x10):
     return _split(vp, seg)
 
 
-def run_both(dev, pkts, cap=65535, can_udp=True, offset=OFFSET):
+def run_both(dev, pkts, cap=65535, can_udp=True, offset=OFFSET, lens_override=None):
     def mk():
         bufs, lens = [], []
         for p in pkts:
@@ -36,6 +36,9 @@ def run_both(dev, pkts, cap=65535, can_udp=True, offset=OFFSET):
             b[offset: offset + len(p)] = np.frombuffer(p, np.uint8)
             bufs.append(b)
             lens.append(offset + len(p))
+        if lens_override:
+            for i, ln in lens_override.items():
+                lens[i] = ln
         return bufs, lens
     bo, lo = mk()
     bp, lp = mk()
@@ -44,6 +47,11 @@ def run_both(dev, pkts, cap=65535, can_udp=True, offset=OFFSET):
     rc_p = 0 if err is None else err.code
     assert rc_p == rc
     if rc:
+        # the loop stopped part-way (gro.go:1335-1337): toWrite so far, the
+        # slice headers and every byte of every buffer as the reference leaves them
+        assert (tw_p, order_p, lens_p) == (tw_o, order_o, lens_o)
+        for i in range(len(bo)):
+            assert np.array_equal(bo[i], bp[i]), f"bufs[{i}] differs after the error"
         return
     assert tw_p == tw_o
     assert order_p == order_o, "prepend swaps differ"
@@ -121,6 +129,20 @@ def test_invalid_offset(dev):
     run_both(dev, s, offset=5)
     tw_p, _, _, err = dev.handle_gro([np.zeros(100, np.uint8)], [10], 12, True)
     assert err is not None and err.code == -4
+
+
+@pytest.mark.parametrize("bad_at", [1, 5, 9, 13])
+def test_invalid_offset_after_coalescing(dev, bad_at):
+    """An invalid offset on a later buffer: the earlier buffers have already
+    been coalesced (appends, prepend swaps, PSH, zero virtio headers of no-op
+    packets) but never applied -- the reference's state at the error."""
+    a = flow(6, seed=21, last_flags=0x18)
+    u = flow(4, udp=True, seed=22)
+    o = flow(4, seed=23)
+    pkts = [a[0], a[1], u[0], o[1], o[0], a[2], u[1], a[3], o[2], a[4], u[2], a[5], o[3], u[3]]
+    icmp = bytearray(a[0]); icmp[9] = 1
+    pkts.insert(3, bytes(icmp))
+    run_both(dev, pkts, lens_override={bad_at: OFFSET})  # len(bufs[bad_at]) == offset: offset > len-1
 
 
 def test_batch_size_128(dev):

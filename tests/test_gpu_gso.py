@@ -256,7 +256,7 @@ def test_general_path_geometries(dev):
     base4 = synth.make_super_packet(6000, 1000, seed=5)
     base6 = synth.make_super_packet(6000, 1000, seed=6, v6=True)
     for cs in (0, 1, 4, 5, 6, 11, 12, 19):  # IPv4 header shorter than 20 bytes (cs == 5: bufs' own byte 5)
-        for co in (6, 16, 40, 65535 - cs + 3):
+        for co in (6, 16, 40, (65536 - cs + 3) % 65536):  # the last wraps the field to position 3
             h = bytearray(base4)
             h[6:8] = cs.to_bytes(2, "little")
             h[8:10] = co.to_bytes(2, "little")

@@ -1,0 +1,114 @@
+"""GPU parity: the Tun.Write stager (wgcs_wstager_*) vs the oracle's
+handleGRO per Write call -- status, toWrite and every byte Tun.Write hands to
+write(2) (bufs[i][offset-10:len] for i in toWrite, tun/tun.go:687-698), for
+many calls batched into one VALIDATE + one coalesce launch, including calls
+whose speculative plan must be redone (invalid checksums), prepends, capacity
+limits, UDP GRO off, and an invalid offset."""
+import numpy as np
+import pytest
+
+import oracle
+from wireguard_amd.tun import WriteStager
+
+from test_gpu_gro import flow
+
+pytestmark = pytest.mark.gpu
+OFFSET = 16
+
+
+def _mk(pkts, cap=65535, offset=OFFSET, lens_override=None):
+    bufs, lens = [], []
+    for p in pkts:
+        b = np.full(cap if isinstance(cap, int) else cap(len(p)), 0x5A, np.uint8)
+        b[offset: offset + len(p)] = np.frombuffer(p, np.uint8)
+        bufs.append(b)
+        lens.append(offset + len(p))
+    for i, ln in (lens_override or {}).items():
+        lens[i] = ln
+    return bufs, lens
+
+
+def _oracle_writes(pkts, cap, can_udp, offset, lens_override):
+    bo, lo = _mk(pkts, cap, offset, lens_override)
+    rc, tw, order, nl = oracle.handle_gro(bo, lo, offset, can_udp)
+    if rc:
+        return rc, [], []
+    return 0, tw, [bo[order[i]][offset - 10: nl[i]].tobytes() for i in tw]
+
+
+def _calls(seed):
+    rng = np.random.default_rng(seed)
+    calls = []
+    for k in range(24):
+        flows = [flow(int(rng.integers(1, 9)), seg=int(rng.choice([536, 1000, 1448])), v6=bool((k + j) % 2),
+                      udp=bool((k + j) % 3 == 0), seed=1000 * seed + 10 * k + j,
+                      last_flags=int(rng.choice([0x10, 0x18]))) for j in range(4)]
+        batch = [p for f in flows for p in f]
+        order = np.argsort(rng.random(len(batch)) + np.arange(len(batch)) * 0.1)
+        pkts = [batch[i] for i in order][:128]
+        cap, can_udp, lo = 65535, True, None
+        if k % 5 == 1:  # bad checksums: the speculative plan is redone for this call
+            for _ in range(3):
+                i = int(rng.integers(0, len(pkts)))
+                b = bytearray(pkts[i]); b[-1] ^= 0x21; pkts[i] = bytes(b)
+        if k % 7 == 2:
+            cap = lambda n: OFFSET + n + 1500  # noqa: E731  room for one more segment only
+        if k % 6 == 3:
+            can_udp = False
+        if k % 11 == 4:
+            lo = {len(pkts) // 2: OFFSET}  # invalid offset part-way: Write writes nothing
+        if k % 4 == 0:  # a prepend: swap two neighbours of one flow
+            f0 = flows[0]
+            if len(f0) >= 2:
+                pkts = [f0[1], f0[0]] + pkts[2:]
+        calls.append((pkts, cap, can_udp, lo))
+    return calls
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_write_stager_matches_handle_gro(dev, seed):
+    calls = _calls(seed)
+    ws = WriteStager(dev, depth=3, max_writes=16, max_pkts=16 * 128, max_bytes=16 * 128 * 1600)
+    pending, expect = [], {}
+    for ci, (pkts, cap, can_udp, lo) in enumerate(calls):
+        bufs, lens = _mk(pkts, cap, OFFSET, lo)
+        try:
+            idx = ws.push(bufs, lens, OFFSET, can_udp)
+        except Exception as e:  # BATCH_FULL: submit the open slot and push again
+            assert getattr(e, "code", None) == -14, e
+            pending.append(ws.submit())
+            idx = ws.push(bufs, lens, OFFSET, can_udp)
+        expect.setdefault(len(pending), []).append((ci, idx, len(pkts)))
+    pending.append(ws.submit())
+    checked = redone = 0
+    for slot_k, batch in enumerate(pending):
+        ws.wait(batch)
+        for ci, idx, n in expect.get(slot_k, []):
+            pkts, cap, can_udp, lo = calls[ci]
+            rc, tw, writes = _oracle_writes(pkts, cap, can_udp, OFFSET, lo)
+            err, tw_p, writes_p = ws.result(batch, idx, n)
+            assert (0 if err is None else err.code) == rc, ci
+            assert tw_p == tw, ci
+            assert writes_p == writes, f"call {ci}: written bytes differ"
+            checked += 1
+    ws.close()
+    assert checked == len(calls)
+
+
+def test_write_stager_ring_reuse(dev):
+    """More slots' worth of calls than the ring holds: every result is read
+    before its slot is recycled (depth - 1 submits later)."""
+    ws = WriteStager(dev, depth=2, max_writes=4, max_pkts=512, max_bytes=512 * 1600)
+    calls = _calls(3)[:12]
+    for r in range(0, len(calls), 4):
+        idxs = []
+        for pkts, cap, can_udp, lo in calls[r: r + 4]:
+            bufs, lens = _mk(pkts, cap, OFFSET, lo)
+            idxs.append(ws.push(bufs, lens, OFFSET, can_udp))
+        b = ws.submit()
+        ws.wait(b)
+        for (pkts, cap, can_udp, lo), idx in zip(calls[r: r + 4], idxs):
+            rc, tw, writes = _oracle_writes(pkts, cap, can_udp, OFFSET, lo)
+            err, tw_p, writes_p = ws.result(b, idx, len(pkts))
+            assert (0 if err is None else err.code, tw_p, writes_p) == (rc, tw, writes)
+    ws.close()

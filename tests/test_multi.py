@@ -9,6 +9,7 @@ import socket
 
 import numpy as np
 import pytest
+import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
@@ -68,6 +69,62 @@ def test_shard_ranges_cover_exactly():
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
             assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1
+
+
+def _worker_mixed(rank, world, port, n_total, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    arena, pkts, lo, hi = shard.mixed_len_shard(n_total, rank, world)
+    valid = oracle.checksum_batch(2, arena, pkts)
+    nbytes = int(pkts["len"].astype(np.int64).sum())
+    t = torch.tensor([nbytes], dtype=torch.int64)
+    dist.all_reduce(t)  # bench-side bookkeeping only (aggregate bytes), not data path
+    q.put((rank, lo, hi, valid.tobytes(), nbytes, int(t.item())))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_mixed_length_shards_are_byte_balanced(world):
+    """Mixed 64..9000-byte frames: the shards are cut by byte prefix sum, each
+    rank's byte count is within one frame of total/world, and the union of the
+    ranks' results is the single-process result."""
+    n_total = 2000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_mixed, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    arena, pkts, _, lens = shard.make_mixed_len_batch(n_total)
+    total = int(lens.sum())
+    assert all(r[5] == total for r in res)
+    assert res[0][1] == 0 and res[-1][2] == n_total and all(res[i][2] == res[i + 1][1] for i in range(world - 1))
+    for r in res:
+        assert abs(r[4] - total / world) <= max(lens), (r[4], total / world)
+    by_bytes = max(abs(r[4] - total / world) for r in res)
+    by_count = max(abs(int(lens[lo:hi].sum()) - total / world)
+                   for lo, hi in (shard.shard_range(n_total, r, world) for r in range(world)))
+    assert by_bytes <= by_count
+    v1 = oracle.checksum_batch(2, arena, pkts)
+    assert b"".join(r[3] for r in res) == v1.tobytes() and v1.all()
+
+
+def test_byte_shards_cover_exactly():
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 7, 1000):
+        lens = rng.integers(1, 9001, size=n)
+        for w in (1, 2, 3, 8):
+            rs = [shard.shard_range_bytes(lens, r, w) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+            if n:
+                b = [int(lens[l:h].sum()) for l, h in rs]
+                assert max(abs(x - lens.sum() / w) for x in b) <= lens.max()
+    assert shard.shard_range_bytes(np.full(1048576, 1500), 3, 8) == shard.shard_range(1048576, 3, 8)
 
 
 def test_shard_is_independent_of_world_size():

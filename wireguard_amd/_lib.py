@@ -118,6 +118,13 @@ def load() -> C.CDLL:
         "wgcs_coalesce_messages": ([vp, u8pp, C.POINTER(sz), C.POINTER(sz), i32, i32, vp, sz, u8pp, C.POINTER(sz),
                                     C.POINTER(sz), C.POINTER(i32), C.POINTER(sz), C.POINTER(i32)], i32),
         "wgcs_stager_copy_out": ([vp, u64, i32, u8pp, C.POINTER(sz), i32, C.POINTER(i32), i32, C.POINTER(i32)], i32),
+        "wgcs_wstager_create": ([vp, u32, u32, u32, sz, C.POINTER(vp)], i32),
+        "wgcs_wstager_destroy": ([vp], i32),
+        "wgcs_wstager_push": ([vp, C.POINTER(vp), C.POINTER(sz), C.POINTER(sz), i32, i32, i32, C.POINTER(i32)], i32),
+        "wgcs_wstager_submit": ([vp, C.POINTER(u64)], i32),
+        "wgcs_wstager_wait": ([vp, u64], i32),
+        "wgcs_wstager_result": ([vp, u64, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(vp),
+                                 C.POINTER(sz)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

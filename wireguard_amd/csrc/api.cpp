@@ -103,6 +103,8 @@ int wgcs_init(int device, wgcs_ctx** out) {
   if (lpp && (atoi(lpp) == 64 || atoi(lpp) == 32)) ctx->tune.lanes_per_pkt = atoi(lpp);
   const char* nt = getenv("WGCS_NT");
   if (nt) ctx->tune.nt = atoi(nt) ? 1 : 0;
+  const char* xc = getenv("WGCS_XCD");
+  if (xc) ctx->tune.xcd = atoi(xc) ? 1 : 0;
   const char* al = getenv("WGCS_ALIGN");
   if (al && (atoi(al) == 16 || atoi(al) == 32 || atoi(al) == 64 || atoi(al) == 128)) ctx->tune.align = atoi(al);
   *out = ctx;

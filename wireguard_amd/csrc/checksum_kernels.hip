@@ -87,14 +87,19 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
                                                              const uint4* __restrict__ pkts,
                                                              const uint64_t* __restrict__ initial,
                                                              uint32_t n, void* __restrict__ out,
-                                                             int inplace, uint32_t amask) {
+                                                             int inplace, uint32_t amask, int xcd) {
   static_assert(G == 16 || G == 32 || G == 64, "group = DPP row, half wave or wave");
   constexpr int PPW = 64 / G;  // packets per wave per step
   const int lane = threadIdx.x & 63;
   const int grp = lane / G;
   const int sub = lane % G;
-  const uint32_t wave =
-      (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+  // XCD-aware order (xcd != 0, grid a multiple of 8): blocks are dealt
+  // round-robin over the 8 XCDs, so logical block (b % 8) * (grid / 8) + b / 8
+  // gives each XCD one contiguous eighth of every grid-stride pass -- frames
+  // that share a 128-B line at their boundary are fetched through one L2.
+  uint32_t blk = blockIdx.x;
+  if (xcd) blk = (blk & 7u) * (gridDim.x >> 3) + (blk >> 3);
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blk * (blockDim.x >> 6) + (threadIdx.x >> 6)));
   const uint32_t step = gridDim.x * (blockDim.x >> 6) * PPW;
   uint4 dn = make_uint4(0, 0, 0, 0);
   {
@@ -224,15 +229,16 @@ static hipError_t launch_mode(uint8_t* arena, const wgcs_pkt* pkts, const uint64
   long cap = (long)num_cu * t.blocks_per_cu;
   const int grid = (int)(want < cap ? want : cap);
   const uint32_t amask = (uint32_t)(t.align >= 16 ? t.align : 16) - 1u;
+  const int xcd = (t.xcd && grid % 8 == 0) ? 1 : 0;
   const uint4* d = reinterpret_cast<const uint4*>(pkts);
 #define WGCS_LAUNCH(G, U)                                                                                    \
   do {                                                                                                      \
     if (t.nt)                                                                                               \
       hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, true>), dim3(grid), dim3(256), 0, s, arena, d,  \
-                         init, n, out, inplace, amask);                                                     \
+                         init, n, out, inplace, amask, xcd);                                                \
     else                                                                                                    \
       hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, false>), dim3(grid), dim3(256), 0, s, arena, d, \
-                         init, n, out, inplace, amask);                                                     \
+                         init, n, out, inplace, amask, xcd);                                                \
   } while (0)
   if (t.lanes_per_pkt == 64) {
     if (t.unroll >= 4) WGCS_LAUNCH(64, 4);

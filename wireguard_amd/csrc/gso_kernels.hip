@@ -603,7 +603,10 @@ __global__ __launch_bounds__(1024) void gso_rows_kernel(const uint8_t* __restric
   const uint4 z = make_uint4(0, 0, 0, 0);
   uint4 A[U];
   uint32_t E = 0;
-  const bool spec = type_s != GSO_NONE && (int64_t)i * gso_s < (int64_t)plen_s;  // row-uniform
+  // RAW jobs split whatever the type byte says (gsoSplit maps non-TCP types to
+  // UDP, gro.go:1398-1405): only handleVirtioRead's GSO_NONE copies one packet
+  const bool splits = type_s != GSO_NONE || (job.flags & WGCS_GSO_JOB_RAW) != 0;
+  const bool spec = splits && (int64_t)i * gso_s < (int64_t)plen_s;  // row-uniform
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const uint8_t* ca = abase + 16 * (r + 16 * u);

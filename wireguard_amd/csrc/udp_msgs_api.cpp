@@ -129,6 +129,10 @@ int wgcs_split_messages(wgcs_ctx* ctx, uint8_t* const* bufs, size_t buf_len, int
                         const size_t* nns, int n_msgs, int first_msg_at, int* addr_src, int* n_packets) {
   if (!ctx || !n_packets) return WGCS_ERR_INVALID_ARG;
   *n_packets = 0;
+  // every message keeps its own Addr unless the split moves one (bind.go:570):
+  // set before any early return, so an error never leaves addr_src unwritten
+  if (addr_src)
+    for (int k = 0; k < n_msgs; ++k) addr_src[k] = k;
   if (n_msgs <= 0 || !bufs || !ns || !addr_src || first_msg_at < 0 || first_msg_at > n_msgs ||
       n_msgs - first_msg_at > 128 ||
       buf_len > 0x7FFFFFFFu || (!oobs && first_msg_at < n_msgs) || (!nns && first_msg_at < n_msgs))

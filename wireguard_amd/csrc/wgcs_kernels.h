@@ -14,6 +14,7 @@ struct LaunchTuning {
   int unroll = 4;          // 16-byte loads in flight per lane per iteration
   int nt = 1;              // non-temporal (streaming) loads: each byte is read once
   int align = 16;          // chunk grid origin: packet start rounded down to this many bytes
+  int xcd = 1;             // XCD-aware block order (each XCD streams contiguous eighths)
 };
 
 hipError_t launch_checksum_batch(int mode, unsigned flags, uint8_t* arena, const wgcs_pkt* pkts,

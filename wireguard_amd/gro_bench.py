@@ -123,22 +123,107 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
         dist.destroy_process_group()
 
 
+def run_staged(args, torch, dev, dist, rank, world, local, barrier, calls_per_slot: int = 64, depth: int = 3):
+    """bench.py --config gro_staged: the Tun.Write stager (wgcs_wstager_*).
+    One step = one ring slot of `calls_per_slot` Write calls (128 packets
+    each, the batch above): push (pinned staging + host flow plan), submit
+    (H2D, one VALIDATE + one coalesce launch, D2H), and -- depth-1 slots later
+    -- wait + per-call results (the write(2) images).  Host buffers in, host
+    buffers out: PCIe-inclusive packets/s."""
+    import ctypes as C
+
+    from .tun import WriteStager
+
+    pkts = make_batch(dev)
+    n = len(pkts)
+    b = Batch(pkts)
+    b.reset()
+    L, h = dev.lib, dev.h
+    ws = WriteStager(dev, depth=depth, max_writes=calls_per_slot, max_pkts=calls_per_slot * n,
+                     max_bytes=calls_per_slot * sum(len(p) + 32 for p in pkts))
+    ptrs = (C.c_void_p * n)(*[C.cast(b.ptrs0[i], C.c_void_p).value for i in range(n)])
+    st, nw = C.c_int(0), C.c_int(0)
+    tw = (C.c_int * n)()
+    outp = (C.c_void_p * n)()
+    outl = (C.c_size_t * n)()
+    idx = C.c_int(0)
+    bt = C.c_uint64(0)
+    inflight = []
+
+    def settle(batch):
+        assert L.wgcs_wstager_wait(ws.h, batch) == 0
+        for k in range(calls_per_slot):
+            L.wgcs_wstager_result(ws.h, batch, k, C.byref(st), C.byref(nw), tw, outp, outl)
+            assert st.value == 0 and nw.value == 4, (st.value, nw.value)
+
+    def step():
+        for _ in range(calls_per_slot):
+            assert L.wgcs_wstager_push(ws.h, ptrs, b.lens0, b.caps, n, OFFSET, 1, C.byref(idx)) == 0
+        if len(inflight) == depth - 1:
+            settle(inflight.pop(0))
+        assert L.wgcs_wstager_submit(ws.h, C.byref(bt)) == 0
+        inflight.append(bt.value)
+
+    for _ in range(max(args.warmup, depth + 1)):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    while inflight:
+        settle(inflight.pop(0))
+    barrier()
+    dt = shard.max_over_ranks(time.perf_counter() - t0, dist)
+    per = dt / args.steps
+    ws.close()
+    # the written images are correct: one slot checked against the oracle in tests/test_gpu_wstager.py
+    result = {
+        "metric": "Tun.Write handleGRO packets/s through the write stager (host buffers in, write(2) images out)",
+        "value": round(calls_per_slot * n * world / per, 1),
+        "unit": "packets/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(per * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{calls_per_slot} Tun.Write calls of 128 TCP/IPv4 packets (4 flows x 32 x 1448-B MSS) per "
+                        f"ring slot, depth {depth}; each call coalesced to 4 super-packets",
+            "packets_per_step": calls_per_slot * n,
+            "payload_bytes_per_step": calls_per_slot * sum(len(p) for p in pkts),
+            "parallelism": f"replica{world} (one stager per GPU, no collective)",
+            "gib_per_s": round(calls_per_slot * sum(len(p) for p in pkts) / per / 2**30, 3),
+        },
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        result["cpu_baseline"] = cpu_baseline(pkts, min(args.cpu_seconds, 5.0))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    dev.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def cpu_baseline(pkts, seconds):
+    """The oracle's handleGRO (C restatement of tun/gro.go) on the same
+    128-packet batch: one core, then all host cores (pthreads,
+    wg_oracle_bench.c); only the calls are timed (not the batch refills)."""
     import os
     import sys
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
     import oracle  # cpu_baseline leg only
 
-    b = Batch(pkts)
-    L = oracle.lib()
-    reps, t_total = 0, 0.0
-    while t_total < seconds:
-        b.reset()
-        t0 = time.perf_counter()
-        L.or_handle_gro(b.ptrs, b.lens, b.caps, b.n, OFFSET, 1, b.tw, b.C.byref(b.ntw))
-        t_total += time.perf_counter() - t0
-        reps += 1
-    return {"value": round(len(pkts) * reps / t_total, 1), "unit": "packets/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} handleGRO calls on the same 128-packet batch, {t_total:.1f} s, "
-                      "C restatement of tun/gro.go, one C call per step (as the product is timed)"}
+    rate1, calls1 = oracle.gro_bench_mt(pkts, OFFSET, True, 1, seconds)
+    threads = oracle.host_threads()
+    rate_mt, calls_mt = oracle.gro_bench_mt(pkts, OFFSET, True, threads, max(seconds / 2, 1.0))
+    return {"value": round(len(pkts) * rate1, 1), "unit": "packets/s", "cores": 1, "kind": "port",
+            "sample": f"{calls1} handleGRO calls on the same {len(pkts)}-packet batch in {seconds:.0f} s, "
+                      "C restatement of tun/gro.go, calls timed (not the refills)",
+            "all_cores": {"value": round(len(pkts) * rate_mt, 1), "unit": "packets/s", "cores": threads,
+                          "host_nproc": os.cpu_count(),
+                          "sample": f"{calls_mt} calls on {threads} pthreads, each on a private copy of the batch"}}

@@ -29,43 +29,57 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
     jobs = np.zeros(n_jobs, GSO_JOB_DTYPE)
     jobs["off"] = np.arange(n_jobs, dtype=np.uint64) * np.uint64(jlen)
     jobs["len"] = jlen
-    stream = torch.cuda.Stream()
+    S = max(1, getattr(args, "streams", 1))
+    streams = [torch.cuda.Stream() for _ in range(S)]
+    R = max(R, 2 * S)
     d_arena = [torch.from_numpy(arena).cuda() for _ in range(R)]
     d_jobs = torch.from_numpy(jobs.view(np.uint8)).cuda()
     d_out = [torch.empty(n_jobs * max_segs * stride, dtype=torch.uint8, device="cuda") for _ in range(R)]
-    d_sizes = torch.zeros(n_jobs * max_segs, dtype=torch.int32, device="cuda")
-    d_count = torch.zeros(n_jobs, dtype=torch.int32, device="cuda")
-    d_status = torch.zeros(n_jobs, dtype=torch.int32, device="cuda")
+    # per-stream result arrays: launches on different streams may overlap
+    d_sizes = [torch.zeros(n_jobs * max_segs, dtype=torch.int32, device="cuda") for _ in range(S)]
+    d_count = [torch.zeros(n_jobs, dtype=torch.int32, device="cuda") for _ in range(S)]
+    d_status = [torch.zeros(n_jobs, dtype=torch.int32, device="cuda") for _ in range(S)]
 
-    def step(k):
-        i = k % R
-        dev.gso_split_batch(d_arena[i], d_jobs, n_jobs, d_out[i], stride, offset, max_segs, d_sizes, d_count,
-                            d_status, stream=stream)
+    def step(k, ns=S):
+        i, q = k % R, k % ns
+        dev.gso_split_batch(d_arena[i], d_jobs, n_jobs, d_out[i], stride, offset, max_segs, d_sizes[q], d_count[q],
+                            d_status[q], stream=streams[q])
 
     for k in range(args.warmup):
         step(k)
     torch.cuda.synchronize()
-    count = d_count.cpu().numpy()
-    status = d_status.cpu().numpy()
+    count = d_count[0].cpu().numpy()
+    status = d_status[0].cpu().numpy()
     assert (status == 0).all() and (count == 45).all(), (status[:4], count[:4])
-    sizes = d_sizes.cpu().numpy().reshape(n_jobs, max_segs)
+    sizes = d_sizes[0].cpu().numpy().reshape(n_jobs, max_segs)
     bytes_out = int(sizes.astype(np.int64).sum())
     bytes_in = int(jobs["len"].astype(np.int64).sum())
     bytes_per_step = bytes_in + bytes_out
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for k in range(args.steps):
-        step(args.warmup + k)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = e0.elapsed_time(e1) / args.steps
+    joins = [torch.cuda.Event() for _ in streams[1:]]
+
+    def timed(K, k0, ns):
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record(streams[0])
+        for st in streams[1:ns]:
+            st.wait_event(e0)
+        for k in range(K):
+            step(k0 + k, ns)
+        for j, st in zip(joins, streams[1:ns]):
+            j.record(st)
+            streams[0].wait_event(j)
+        e1.record(streams[0])
+        torch.cuda.synchronize()
+        barrier()
+        return time.perf_counter() - t0, e0.elapsed_time(e1) / K
+
+    elapsed, kern_ms = timed(args.steps, args.warmup, S)
     elapsed = shard.max_over_ranks(elapsed, dist)
+    iso_ms = timed(max(args.steps, 20), args.warmup + args.steps, 1)[1] if S > 1 else None
+    stream = streams[0]
     achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
     # calibration: a plain device-to-device copy of the super-packet bytes
     # (same read + write volume, same rotation) with the runtime's copy kernel
@@ -100,6 +114,7 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
             "bytes_in": bytes_in,
             "bytes_out": bytes_out,
             "rotated_copies": R,
+            "streams": S,
             "parallelism": f"shard{world} (no collective)",
         },
         "roofline": {
@@ -111,10 +126,15 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
             "traffic": traffic.per_launch("gso_rows_kernel<6,true>", bytes_per_step),
             "kernel": "gso_rows_kernel<6,true>",
             "kernel_ms": round(kern_ms, 5),
+            "kernel_ms_is": ("GPU time per launch over the timed region (HIP events on the launch streams)"
+                             + (f"; {S} streams, consecutive launches overlap" if S > 1 else "")),
             "algorithmic_bytes_per_launch": bytes_per_step,
             "d2d_copy_same_bytes_ms": round(copy_ms, 5),
         },
     }
+    if iso_ms is not None:
+        result["roofline"]["kernel_ms_one_stream"] = round(iso_ms, 5)
+        result["roofline"]["frac_one_stream"] = round(bytes_per_step / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     if not getattr(args, "no_e2e", False):
         result["end_to_end"] = end_to_end(dev, pkts, bytes_in, bytes_out, steps=max(10, min(args.steps, 40)))
         result["host_call"] = host_call(dev, pkts[0], with_cpu=rank == 0 and world == 1 and args.cpu_seconds > 0)
@@ -207,19 +227,22 @@ def host_call(dev, vp: bytes, with_cpu: bool, reps: int = 200):
 
 
 def cpu_baseline(pkts, seconds, bytes_per_step):
+    """The oracle's handleVirtioRead (C restatement of tun/tun.go:514-632 +
+    gsoSplit) over the same 256 reads: one core for `seconds`, then all host
+    cores (pthreads, wg_oracle_bench.c) for a quarter of that."""
     import os
     import sys
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
     import oracle  # cpu_baseline leg only
 
-    bufs = [np.zeros(1536, np.uint8) for _ in range(64)]
-    reps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        for p in pkts:
-            rb = np.frombuffer(bytearray(p), np.uint8)
-            oracle.handle_virtio_read(rb, bufs, 16)
-        reps += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(bytes_per_step * reps / dt / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} passes over the 256 super-packets, {dt:.1f} s, C restatement of handleVirtioRead+gsoSplit"}
+    per_read = bytes_per_step / len(pkts)
+    rate1, calls1 = oracle.gso_bench_mt(pkts, 64, 1536, 16, 1, seconds)
+    threads = oracle.host_threads()
+    rate_mt, calls_mt = oracle.gso_bench_mt(pkts, 64, 1536, 16, threads, max(seconds / 4, 1.0))
+    return {"value": round(per_read * rate1 / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{calls1} handleVirtioRead calls over the 256 super-packets in {seconds:.0f} s, C restatement "
+                      "of tun/tun.go:514-632 + gsoSplit, 1 thread, calls timed (not the readBuf refills)",
+            "all_cores": {"value": round(per_read * rate_mt / 2**30, 3), "unit": "GiB/s", "cores": threads,
+                          "host_nproc": os.cpu_count(),
+                          "sample": f"{calls_mt} calls on {threads} pthreads, each on private copies"}}

@@ -26,11 +26,70 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return n * rank // world, n * (rank + 1) // world
 
 
+def shard_range_bytes(lens, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous [lo, hi) packet range of `rank` balanced by BYTES (mixed
+    lengths): the cuts are the packet boundaries nearest to the prefix-sum
+    targets k * total / world, so each rank's bytes differ from total / world
+    by at most one packet.  Equal lengths give shard_range."""
+    assert 0 <= rank < world
+    cum = np.concatenate([[0], np.cumsum(np.asarray(lens, dtype=np.int64))])
+    total = int(cum[-1])
+
+    def cut(r):
+        if r == 0:
+            return 0
+        if r == world:
+            return len(cum) - 1
+        t = total * r // world
+        i = int(np.searchsorted(cum, t, side="left"))
+        if i > 0 and t - cum[i - 1] < cum[i] - t:
+            i -= 1
+        return i
+
+    return cut(rank), cut(rank + 1)
+
+
+LEN_CHOICES = (64, 576, 1280, 1500, 4096, 9000)
+
+
+def make_mixed_len_batch(n: int, seed: int = synth.SEED):
+    """n seeded frames of mixed kinds AND mixed lengths (LEN_CHOICES), packed
+    back to back; returns (arena, pkts, kinds, lens)."""
+    rng = np.random.default_rng(seed)
+    lens = rng.choice(np.array(LEN_CHOICES, np.int64), size=n)
+    kinds = rng.integers(0, 4, size=n)
+    kinds[(lens < 64)] = synth.KIND_UDP4
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    arena = np.zeros(int(lens.sum()) + 64, np.uint8)
+    for L in np.unique(lens):
+        idx = np.nonzero(lens == L)[0]
+        fr = synth.build_frames(kinds[idx], int(L), rng)
+        for j, i in enumerate(idx):
+            arena[int(offs[i]): int(offs[i]) + int(L)] = fr[j]
+    pkts = synth.describe(kinds, lens, offs)
+    return arena, pkts, kinds, lens
+
+
+def mixed_len_shard(n_total: int, rank: int, world: int, seed: int = synth.SEED):
+    """Rank's byte-balanced shard of make_mixed_len_batch(n_total): (arena,
+    pkts rebased to the shard's arena, lo, hi)."""
+    arena, pkts, _, lens = make_mixed_len_batch(n_total, seed)
+    lo, hi = shard_range_bytes(lens, rank, world)
+    from .tun import pkt_off, set_pkt_off
+
+    offs = pkt_off(pkts)
+    a0 = int(offs[lo]) if lo < n_total else len(arena) - 64
+    a1 = int(offs[hi - 1]) + int(lens[hi - 1]) if hi > lo else a0
+    sub = pkts[lo:hi].copy()
+    set_pkt_off(sub, offs[lo:hi] - np.uint64(a0))
+    return np.concatenate([arena[a0:a1], np.zeros(64, np.uint8)]), sub, lo, hi
+
+
 def make_global_shard(n_total: int, rank: int, world: int, frame_len: int = 1500, kinds: str = "mixed",
                       seed: int = synth.SEED, chunk: int = CHUNK):
     """Packets [lo, hi) of the seeded global batch of n_total frames.
     Returns (arena, pkts, kinds, lo, hi) with offsets local to the arena."""
-    lo, hi = shard_range(n_total, rank, world)
+    lo, hi = shard_range_bytes(np.full(n_total, frame_len, np.int64), rank, world)
     parts, kparts = [], []
     c0 = lo // chunk
     for c in range(c0, (hi + chunk - 1) // chunk):

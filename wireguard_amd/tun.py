@@ -53,7 +53,7 @@ VIRTIO_NET_HDR_GSO_TCPV6 = 4
 VIRTIO_NET_HDR_GSO_UDP_L4 = 5
 
 __all__ = [
-    "Device", "Stager", "PKT_DTYPE", "GSO_JOB_DTYPE", "MODE_FOLD", "MODE_L4_FILL", "MODE_VALIDATE", "MODE_PARTIAL",
+    "Device", "Stager", "WriteStager", "PKT_DTYPE", "GSO_JOB_DTYPE", "MODE_FOLD", "MODE_L4_FILL", "MODE_VALIDATE", "MODE_PARTIAL",
     "MODE_IP4HDR", "F_INPLACE", "PKT_V6", "IPPROTO_TCP", "IPPROTO_UDP", "VirtioHdr", "WgcsError", "set_pkt_off",
     "pkt_off",
 ]
@@ -302,3 +302,58 @@ class Stager:
             self.dev._check(rc)
         sizes[: len(bufs)] = list(csz)
         return n.value, self.dev._err(rc)
+
+
+class WriteStager:
+    """Tun.Write batch staging ring (include/wgcsum.h wgcs_wstager_*): many
+    Write calls -> one VALIDATE + one coalesce launch, pipelined H2D / kernels /
+    D2H.  push(bufs, lens, offset) stages one Write call (bufs: numpy arrays of
+    cap(bufs[i]) bytes holding len lens[i], the packet at [offset:lens[i]]);
+    result() returns what Tun.Write would write(2) for it (tun/tun.go:687-698)."""
+
+    def __init__(self, dev: Device, depth: int, max_writes: int, max_pkts: int, max_bytes: int):
+        self.dev, self.lib = dev, dev.lib
+        h = C.c_void_p()
+        dev._check(self.lib.wgcs_wstager_create(dev.h, depth, max_writes, max_pkts, max_bytes, C.byref(h)))
+        self.h = h
+        self._n = {}
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.wgcs_wstager_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def push(self, bufs: list, lens: list, offset: int, can_udp_gro: bool = True) -> int:
+        n = len(bufs)
+        ptrs = (C.c_void_p * max(n, 1))(*[b.ctypes.data for b in bufs])
+        cl = (C.c_size_t * max(n, 1))(*lens)
+        cc = (C.c_size_t * max(n, 1))(*[len(b) for b in bufs])
+        idx = C.c_int(0)
+        self.dev._check(self.lib.wgcs_wstager_push(self.h, ptrs, cl, cc, n, offset, int(can_udp_gro), C.byref(idx)))
+        return idx.value
+
+    def submit(self) -> int:
+        b = C.c_uint64(0)
+        self.dev._check(self.lib.wgcs_wstager_submit(self.h, C.byref(b)))
+        return b.value
+
+    def wait(self, batch: int) -> None:
+        self.dev._check(self.lib.wgcs_wstager_wait(self.h, batch))
+
+    def result(self, batch: int, write_idx: int, n: int):
+        """(err, to_write, packets): packets[k] = bytes written for to_write[k]
+        (virtio header + packet), err a WgcsError or None."""
+        st, nw = C.c_int(0), C.c_int(0)
+        m = max(n, 1)
+        tw = (C.c_int * m)()
+        ps = (C.c_void_p * m)()
+        pl = (C.c_size_t * m)()
+        self.dev._check(self.lib.wgcs_wstager_result(self.h, batch, write_idx, C.byref(st), C.byref(nw), tw, ps, pl))
+        pkts = [C.string_at(ps[k], pl[k]) for k in range(nw.value)]
+        return self.dev._err(st.value), list(tw)[: nw.value], pkts
