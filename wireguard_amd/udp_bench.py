@@ -40,22 +40,38 @@ def _gro_cmsg(g):
         int(g).to_bytes(2, "little") + bytes(6)
 
 
-def _time_steps(torch, stream, step, steps, warmup, barrier):
+def _time_steps(torch, streams, step, steps, warmup, barrier):
+    """Step k runs on streams[k % S] (consecutive batches are independent);
+    returns (wall seconds, GPU ms per launch over the timed region, the same
+    on one stream or None)."""
+    S = len(streams)
     for k in range(warmup):
-        step(k)
+        step(k, S)
     torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for k in range(steps):
-        step(warmup + k)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    barrier()
-    return time.perf_counter() - t0, e0.elapsed_time(e1) / steps
+    joins = [torch.cuda.Event() for _ in streams[1:]]
+
+    def timed(K, k0, ns):
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record(streams[0])
+        for st in streams[1:ns]:
+            st.wait_event(e0)
+        for k in range(K):
+            step(k0 + k, ns)
+        for j, st in zip(joins, streams[1:ns]):
+            j.record(st)
+            streams[0].wait_event(j)
+        e1.record(streams[0])
+        torch.cuda.synchronize()
+        barrier()
+        return time.perf_counter() - t0, e0.elapsed_time(e1) / K
+
+    el, ms = timed(steps, warmup, S)
+    iso = timed(max(steps, 10), warmup + steps, 1)[1] if S > 1 else None
+    return el, ms, iso
 
 
 def _copy_ms(torch, stream, dsts, srcs, nbytes, steps):
@@ -94,18 +110,26 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
         dist.destroy_process_group()
 
 
-def _result(metric, args, workload, extra, kname, kern_ms, bps, copy_ms, elapsed):
+def _result(metric, args, workload, extra, kname, kern_ms, bps, copy_ms, elapsed, iso_ms=None, S=1):
     achieved = bps / (kern_ms * 1e-3) / 1e9
-    return {
+    res = {
         "metric": metric, "value": None, "unit": "GiB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic", "config": {"workload": workload, **extra},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic.per_launch(kname, bps), "kernel": kname,
-                     "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_launch": bps,
+                     "kernel_ms": round(kern_ms, 5),
+                     "kernel_ms_is": ("GPU time per launch over the timed region (HIP events on the launch streams)"
+                                      + (f"; {S} streams, consecutive launches overlap" if S > 1 else "")),
+                     "algorithmic_bytes_per_launch": bps,
                      "d2d_copy_same_bytes_ms": round(copy_ms, 5)},
         "_elapsed": elapsed,
     }
+    res["config"]["streams"] = S
+    if iso_ms is not None:
+        res["roofline"]["kernel_ms_one_stream"] = round(iso_ms, 5)
+        res["roofline"]["frac_one_stream"] = round(bps / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    return res
 
 
 # --------------------------------------------------------------------- split
@@ -120,7 +144,10 @@ def run_split(args, torch, dev, rank, world, barrier, B=1024, n_msgs=128, first=
     for b in range(B):
         n_in[b * n_msgs + first: (b + 1) * n_msgs] = SEGS * MSG
         gso[b * n_msgs + first: (b + 1) * n_msgs] = MSG
-    stream = torch.cuda.Stream()
+    S = max(1, getattr(args, "streams", 1))
+    streams = [torch.cuda.Stream() for _ in range(S)]
+    stream = streams[0]
+    R = max(R, S)
     d_in = []
     for _ in range(R):
         t = torch.zeros((B * ns, in_stride), dtype=torch.uint8, device="cuda")
@@ -128,21 +155,23 @@ def run_split(args, torch, dev, rank, world, barrier, B=1024, n_msgs=128, first=
         d_in.append(t)
     d_n, d_g = torch.from_numpy(n_in).cuda(), torch.from_numpy(gso).cuda()
     d_out = [torch.empty((B * n_msgs, out_stride), dtype=torch.uint8, device="cuda") for _ in range(R)]
-    d_nout = torch.zeros(B * n_msgs, dtype=torch.int32, device="cuda")
-    d_src = torch.zeros(B * n_msgs, dtype=torch.int32, device="cuda")
-    d_cnt = torch.zeros(B, dtype=torch.int32, device="cuda")
-    d_st = torch.zeros(B, dtype=torch.int32, device="cuda")
-    L, h, s = dev.lib, dev.h, stream.cuda_stream
+    # per-stream result arrays: launches on different streams may overlap
+    d_nout = [torch.zeros(B * n_msgs, dtype=torch.int32, device="cuda") for _ in range(S)]
+    d_src = [torch.zeros(B * n_msgs, dtype=torch.int32, device="cuda") for _ in range(S)]
+    d_cnt = [torch.zeros(B, dtype=torch.int32, device="cuda") for _ in range(S)]
+    d_st = [torch.zeros(B, dtype=torch.int32, device="cuda") for _ in range(S)]
+    L, h = dev.lib, dev.h
 
-    def step(k):
-        i = k % R
+    def step(k, ns):
+        i, q = k % R, k % ns
         rc = L.wgcs_split_messages_batch(h, d_in[i].data_ptr(), in_stride, buf_len, d_n.data_ptr(), d_g.data_ptr(),
-                                         n_msgs, first, B, d_out[i].data_ptr(), out_stride, d_nout.data_ptr(),
-                                         d_src.data_ptr(), d_cnt.data_ptr(), d_st.data_ptr(), s)
+                                         n_msgs, first, B, d_out[i].data_ptr(), out_stride, d_nout[q].data_ptr(),
+                                         d_src[q].data_ptr(), d_cnt[q].data_ptr(), d_st[q].data_ptr(),
+                                         streams[q].cuda_stream)
         assert rc == 0
 
-    elapsed, kern_ms = _time_steps(torch, stream, step, args.steps, args.warmup, barrier)
-    cnt, st = d_cnt.cpu().numpy(), d_st.cpu().numpy()
+    elapsed, kern_ms, iso_ms = _time_steps(torch, streams, step, args.steps, args.warmup, barrier)
+    cnt, st = d_cnt[0].cpu().numpy(), d_st[0].cpu().numpy()
     assert (st == 0).all() and (cnt == ns * SEGS).all(), (st[:4], cnt[:4])
     # size-independent property: packet k of batch b is bytes [k*1452, +1452) of its datagram
     out = d_out[0].view(B, n_msgs, out_stride)
@@ -157,7 +186,7 @@ def run_split(args, torch, dev, rank, world, barrier, B=1024, n_msgs=128, first=
                   f"{SEGS} x {MSG}-B transport messages each -> {ns * SEGS} packets per batch; splitMessages, "
                   "conn/bind.go:542-597 (SURVEY.md §8f row 3)",
                   {"batches": B, "packets_per_step": B * ns * SEGS, "payload_bytes": payload, "rotated_copies": R},
-                  "udp_split_kernel<6>", kern_ms, bps, copy_ms, elapsed)
+                  "udp_split_kernel<6>", kern_ms, bps, copy_ms, elapsed, iso_ms, S)
     if rank == 0 and world == 1 and not getattr(args, "no_e2e", False):
         res["host_call"] = split_host_call(dev, with_cpu=args.cpu_seconds > 0)
         if args.cpu_seconds > 0:
@@ -264,9 +293,11 @@ def run_coalesce(args, torch, dev, rank, world, barrier, B=1024, max_bufs=128):
 
     stride, cap = int(os.environ.get("WGCS_UDP_STRIDE", 65536)), 65535
     rng = np.random.default_rng(synth.SEED + 88 + rank)
-    R = 2
+    S = max(1, getattr(args, "streams", 1))
+    streams = [torch.cuda.Stream() for _ in range(S)]
+    stream = streams[0]
+    R = max(2, S)
     pk = rng.integers(0, 256, (B * max_bufs, MSG), dtype=np.uint8)
-    stream = torch.cuda.Stream()
     d_bufs = []
     for _ in range(R):
         t = torch.zeros((B * max_bufs, stride), dtype=torch.uint8, device="cuda")
@@ -274,22 +305,23 @@ def run_coalesce(args, torch, dev, rank, world, barrier, B=1024, max_bufs=128):
         d_bufs.append(t)
     d_lens = torch.full((B * max_bufs,), MSG, dtype=torch.int32, device="cuda")
     d_nb = torch.full((B,), max_bufs, dtype=torch.int32, device="cuda")
-    d_nm = torch.zeros(B, dtype=torch.int32, device="cuda")
-    d_first, d_len, d_gso = (torch.zeros(B * max_bufs, dtype=torch.int32, device="cuda") for _ in range(3))
-    L, h, s = dev.lib, dev.h, stream.cuda_stream
+    d_nm = [torch.zeros(B, dtype=torch.int32, device="cuda") for _ in range(S)]
+    d_first, d_len, d_gso = ([torch.zeros(B * max_bufs, dtype=torch.int32, device="cuda") for _ in range(S)]
+                             for _ in range(3))
+    L, h = dev.lib, dev.h
 
-    def step(k):
-        i = k % R
+    def step(k, ns):
+        i, q = k % R, k % ns
         rc = L.wgcs_coalesce_messages_batch(h, d_bufs[i].data_ptr(), stride, cap, None, d_lens.data_ptr(),
-                                            d_nb.data_ptr(), max_bufs, B, 0, d_nm.data_ptr(), d_first.data_ptr(),
-                                            d_len.data_ptr(), d_gso.data_ptr(), s)
+                                            d_nb.data_ptr(), max_bufs, B, 0, d_nm[q].data_ptr(), d_first[q].data_ptr(),
+                                            d_len[q].data_ptr(), d_gso[q].data_ptr(), streams[q].cuda_stream)
         assert rc == 0
 
-    elapsed, kern_ms = _time_steps(torch, stream, step, args.steps, args.warmup, barrier)
-    nm = d_nm.cpu().numpy()
+    elapsed, kern_ms, iso_ms = _time_steps(torch, streams, step, args.steps, args.warmup, barrier)
+    nm = d_nm[0].cpu().numpy()
     assert (nm == 3).all(), nm[:4]
     runs = [SEGS, SEGS, max_bufs - 2 * SEGS]
-    ml = d_len.view(B, max_bufs)[:, :3].cpu().numpy()
+    ml = d_len[0].view(B, max_bufs)[:, :3].cpu().numpy()
     assert (ml == np.array(runs) * MSG).all()
     for b in (0, B // 2, B - 1):  # the first buffer of run r holds packets f..f+n-1 back to back
         f = 0
@@ -307,7 +339,7 @@ def run_coalesce(args, torch, dev, rank, world, barrier, B=1024, max_bufs=128):
                   "conn/bind.go:599-662, in place (SURVEY.md §8f row 3)",
                   {"batches": B, "packets_per_step": B * max_bufs, "moved_bytes": moved, "rotated_copies": R,
                    "slot_stride": stride},
-                  "udp_coalesce_kernel<6,16>", kern_ms, bps, copy_ms, elapsed)
+                  "udp_coalesce_kernel<6,16>", kern_ms, bps, copy_ms, elapsed, iso_ms, S)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         res["cpu_baseline"] = coalesce_cpu_baseline(pk, args.cpu_seconds)
     return res
