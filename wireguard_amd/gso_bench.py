@@ -25,7 +25,7 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
     R = max(args.rotate, 8)  # (16.8 MB in + 25 MB out) per copy: rotate past the 256 MiB MALL
     pkts = [synth.make_super_packet(total, gso, seed=synth.SEED + 1000 * rank + k) for k in range(n_jobs)]
     jlen = len(pkts[0])
-    arena = np.frombuffer(b"".join(pkts), dtype=np.uint8).copy()
+    arena = np.frombuffer(b"".join(pkts) + bytes(64), dtype=np.uint8).copy()  # 64 B of slack past the last job
     jobs = np.zeros(n_jobs, GSO_JOB_DTYPE)
     jobs["off"] = np.arange(n_jobs, dtype=np.uint64) * np.uint64(jlen)
     jobs["len"] = jlen
