@@ -42,7 +42,7 @@ using namespace wgcs::gro;
 
 namespace {
 
-constexpr size_t kHead = 16;  // headroom before each staged packet: its zero virtio header goes there
+constexpr size_t kHead = 16;  // headroom before each staged packet: its virtio header bytes go there
 
 inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -283,7 +283,12 @@ int wgcs_wstager_push(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t
   for (int i = 0; i < n_eff; ++i) {
     const size_t pl = lens[i] - (size_t)offset;
     const uint64_t at = s.used + kHead;
-    memset(s.h_stage + s.used, 0, kHead);  // the zero virtio header a NOOP / INSERT packet is written with
+    // headroom: the caller's bytes bufs[i][offset-10:offset].  A buffer whose
+    // table item was dropped (tcpGRO's deleteAt after coalesceItemInvalidChecksum,
+    // gro.go:942-945) is written with them, as no virtio header is ever encoded
+    // into it; NOOP and unmerged items get a zero header at settle (wait).
+    memset(s.h_stage + s.used, 0, kHead - kVnetLen);
+    memcpy(s.h_stage + at - kVnetLen, bufs[i] + offset - kVnetLen, kVnetLen);
     memcpy(s.h_stage + at, bufs[i] + offset, pl);
     b.stage[i] = at;
     s.used = at + al16(pl);
@@ -408,6 +413,13 @@ int wgcs_wstager_wait(wgcs_wstager* ws, uint64_t batch) {
     if (e == hipSuccess) e = hipMemcpyAsync(s->h_fix, s->d_fix, fix_out, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     if (e != hipSuccess) return hip_fail(ws->ctx, e, "wstager re-plan");
+  }
+  // the zero virtio header of NOOP buffers (gro.go:1350-1356) and of unmerged
+  // items (applyTCPCoalesce / applyUDPCoalesce, gro.go:1168-1174), into the
+  // staged headroom of the buffer now at that slot (H2D is long done)
+  for (const WBatch& b : s->batches) {
+    if (b.status) continue;
+    for (int slot : b.plan.zero_hdr) memset(s->h_stage + b.stage[b.order[slot]] - kVnetLen, 0, kVnetLen);
   }
   s->state = 3;
   return WGCS_OK;
