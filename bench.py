@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--mode", default="validate", choices=["validate", "fill"])
     ap.add_argument("--rotate", type=int, default=4, help="distinct batch copies (defeat the 256 MiB MALL)")
     ap.add_argument("--streams", type=int, default=0,
-                    help="launch streams, consecutive batches round-robin (0: 2, or 1 for the launch-bound cfg1)")
+                    help="launch streams, consecutive batches round-robin (0: 2; 1 for the launch-bound cfg1 and for cfg5, whose 0.26-ms launches gain nothing from overlapping boundaries)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-event-timing", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end measurement")
@@ -72,7 +72,7 @@ def parse():
 def main():
     args = parse()
     if args.streams <= 0:
-        args.streams = 1 if args.config == "cfg1" else 2
+        args.streams = 1 if args.config in ("cfg1", "cfg5") else 2
     import torch  # before wireguard_amd: one HIP runtime per process
 
     from wireguard_amd import shard, synth, traffic
@@ -277,9 +277,9 @@ def _tune_tag():
 def end_to_end(torch, dev, arena_np, pkts_np, mode, barrier, dist, red_dev, world, iters=10, chunks=8):
     """Host -> device -> host rate (the path starts and ends in host memory,
     tun/tun.go:490, :688): pinned H2D of the batch, the kernel, D2H of the
-    per-packet results, double-buffered -- the batch goes in `chunks` pieces
-    alternating over two streams, so chunk k+1's H2D overlaps chunk k's kernel
-    and D2H.  Every rank runs it at once on its own GPU and PCIe link; the
+    per-packet results, pipelined -- the batch goes in `chunks` pieces whose
+    H2D copies run back to back on a copy stream, so chunk k+1's H2D overlaps
+    chunk k's kernel and D2H on the compute stream.  Every rank runs it at once on its own GPU and PCIe link; the
     aggregate is all ranks' bytes over the slowest rank's time."""
     from wireguard_amd import tun
 
@@ -303,33 +303,49 @@ def end_to_end(torch, dev, arena_np, pkts_np, mode, barrier, dist, red_dev, worl
         sub = pkts_np[lo:hi].copy()
         tun.set_pkt_off(sub, offs[lo:hi] - np.uint64(a0))
         parts.append((lo, hi, a0, a1, torch.from_numpy(sub.view(np.uint8)).to("cuda")))
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    copy_s, comp_s = torch.cuda.Stream(), torch.cuda.Stream()
+    evs = [torch.cuda.Event() for _ in parts]
     torch.cuda.synchronize()
 
-    def one_batch():
+    def pipelined():  # H2D chunks back to back on one copy stream; kernel + D2H of chunk k once it has landed
         for k, (lo, hi, a0, a1, d_p) in enumerate(parts):
-            s = streams[k & 1]
-            with torch.cuda.stream(s):
+            with torch.cuda.stream(copy_s):
                 d_arena[a0:a1].copy_(h_arena[a0:a1], non_blocking=True)
-                dev.checksum_batch(mode, d_arena[a0:], d_p, hi - lo, d_out[lo * out_b:], stream=s)
+                evs[k].record(copy_s)
+            comp_s.wait_event(evs[k])
+            with torch.cuda.stream(comp_s):
+                dev.checksum_batch(mode, d_arena[a0:], d_p, hi - lo, d_out[lo * out_b:], stream=comp_s)
                 h_out[lo * out_b: hi * out_b].copy_(d_out[lo * out_b: hi * out_b], non_blocking=True)
 
-    for _ in range(2):
-        one_batch()
-    torch.cuda.synchronize()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        one_batch()
-    torch.cuda.synchronize()
-    barrier()
+    def serialized():  # whole batch: H2D, kernel, D2H on one stream
+        with torch.cuda.stream(comp_s):
+            d_arena.copy_(h_arena, non_blocking=True)
+            dev.checksum_batch(mode, d_arena, d_pkts_all, n, d_out, stream=comp_s)
+            h_out[: n * out_b].copy_(d_out[: n * out_b], non_blocking=True)
+
+    d_pkts_all = torch.from_numpy(pkts_np.view(np.uint8)).to("cuda")
     from wireguard_amd import shard
 
-    dt = shard.max_over_ranks((time.perf_counter() - t0) / iters, dist, device=red_dev)
+    def timed(fn):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        barrier()
+        return shard.max_over_ranks((time.perf_counter() - t0) / iters, dist, device=red_dev)
+
+    dt = timed(pipelined)
+    dt_ser = timed(serialized)
     return {"value": round(world * nbytes / dt / 2**30, 2), "unit": "GiB/s", "ms_per_batch": round(dt * 1e3, 4),
-            "n_gpus": world,
-            "what": f"pinned H2D of the batch + kernel + D2H of the per-packet results, {len(parts)} chunks "
-                    "double-buffered over two streams, every rank at once (aggregate; PCIe bound)"}
+            "n_gpus": world, "serialized_GiB_per_s": round(world * nbytes / dt_ser / 2**30, 2),
+            "what": f"pinned H2D of the batch + kernel + D2H of the per-packet results, {len(parts)} chunks: "
+                    "H2D back to back on a copy stream, each chunk's kernel + D2H on a compute stream once it "
+                    "has landed; every rank at once (aggregate; PCIe bound). serialized_GiB_per_s: the whole "
+                    "batch H2D -> kernel -> D2H on one stream"}
 
 
 def host_call(dev, arena_np, pkts_np, mode, reps=50):

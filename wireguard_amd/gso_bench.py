@@ -158,9 +158,12 @@ def end_to_end(dev, pkts, bytes_in, bytes_out, steps: int, depth: int = 3):
     st = Stager(dev, depth=depth, max_reads=len(arrs), max_bytes=sum(len(a) + 16 for a in arrs), max_segs=64,
                 seg_room=1536 - 16)
     inflight = []
+    push_t = [0.0]
 
     def one():
+        t = time.perf_counter()
         st.push_many(arrs)
+        push_t[0] += time.perf_counter() - t
         if len(inflight) == depth - 1:  # the next submit recycles the oldest slot: consume it first
             b = inflight.pop(0)
             st.wait(b)
@@ -170,6 +173,7 @@ def end_to_end(dev, pkts, bytes_in, bytes_out, steps: int, depth: int = 3):
 
     for _ in range(depth + 2):
         one()
+    push_t[0] = 0.0
     t0 = time.perf_counter()
     for _ in range(steps):
         one()
@@ -179,6 +183,7 @@ def end_to_end(dev, pkts, bytes_in, bytes_out, steps: int, depth: int = 3):
     st.close()
     return {"value": round((bytes_in + bytes_out) / dt / 2**30, 2), "unit": "GiB/s",
             "ms_per_batch": round(dt * 1e3, 4), "bytes_in_plus_out": bytes_in + bytes_out,
+            "host_push_ms_per_batch": round(push_t[0] / steps * 1e3, 4),
             "what": f"Tun.Read stager, depth {depth}: host memcpy of the reads into pinned staging + H2D + "
                     "split kernel + D2H of the packed segments (PCIe-inclusive)"}
 

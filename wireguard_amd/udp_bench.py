@@ -14,6 +14,7 @@ moves once: the first buffer of a coalesced run stays where it is).
 from __future__ import annotations
 
 import json
+import os
 import time
 
 import numpy as np
@@ -247,9 +248,38 @@ def split_host_call(dev, with_cpu: bool, reps: int = 200):
     return out
 
 
+def _threaded_rate(make_pass, threads, seconds):
+    """All-cores leg: `threads` Python threads, each running passes of its own
+    state (make_pass() -> (one_pass, bytes_per_pass)); the oracle's C calls
+    release the GIL (ctypes), so the threads run on separate cores.  Rate =
+    sum over threads of bytes / time inside its passes."""
+    import threading
+
+    out = [None] * threads
+    go = threading.Barrier(threads)
+
+    def work(t):
+        one, nbytes = make_pass()
+        go.wait()
+        busy, reps, t_end = 0.0, 0, time.perf_counter() + seconds
+        while time.perf_counter() < t_end:
+            t0 = time.perf_counter()
+            one()
+            busy += time.perf_counter() - t0
+            reps += 1
+        out[t] = (nbytes * reps / busy if busy > 0 else 0.0, reps)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    return sum(r for r, _ in out), sum(n for _, n in out)
+
+
 def split_cpu_baseline(srcs, seconds, B=16, n_msgs=128, first=126):
     """The oracle (C restatement of splitMessages) on B batches of the same
-    shape, 1 thread, for `seconds`."""
+    shape: 1 thread for `seconds`, then every host thread (all_cores)."""
     import ctypes as C
 
     oracle = _oracle()
@@ -258,33 +288,39 @@ def split_cpu_baseline(srcs, seconds, B=16, n_msgs=128, first=126):
                                  C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
     L.or_split_batch.restype = None
     ns_ = n_msgs - first
-    bufs = np.zeros((B * n_msgs, 65535), np.uint8)
-    ns0 = np.zeros(B * n_msgs, np.int32)
-    oobs = np.zeros((B * n_msgs, 24), np.uint8)
-    nns = np.zeros(B * n_msgs, np.int32)
-    for b in range(B):
-        for t in range(ns_):
-            q = b * n_msgs + first + t
-            bufs[q, : SEGS * MSG] = srcs[b * ns_ + t]
-            ns0[q] = SEGS * MSG
-            oobs[q] = np.frombuffer(_gro_cmsg(MSG), np.uint8)
-            nns[q] = 24
-    cnt = np.zeros(B, np.int32)
-    st = np.zeros(B, np.int32)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        ns = ns0.copy()
-        L.or_split_batch(bufs.ctypes.data, 65535, 65535, ns.ctypes.data, oobs.ctypes.data, 24, nns.ctypes.data,
-                         n_msgs, first, B, cnt.ctypes.data, st.ctypes.data)
-        reps += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    assert (cnt == ns_ * SEGS).all() and (st == 0).all()
     bps = 2 * B * ns_ * SEGS * MSG
-    return {"value": round(bps * reps / dt / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} passes over {B} recvmmsg batches of the same shape, {dt:.1f} s, "
-                      "C restatement of splitMessages (bytes read + written)"}
+
+    def make_pass():
+        bufs = np.zeros((B * n_msgs, 65535), np.uint8)
+        ns0 = np.zeros(B * n_msgs, np.int32)
+        oobs = np.zeros((B * n_msgs, 24), np.uint8)
+        nns = np.zeros(B * n_msgs, np.int32)
+        for b in range(B):
+            for t in range(ns_):
+                q = b * n_msgs + first + t
+                bufs[q, : SEGS * MSG] = srcs[b * ns_ + t]
+                ns0[q] = SEGS * MSG
+                oobs[q] = np.frombuffer(_gro_cmsg(MSG), np.uint8)
+                nns[q] = 24
+        cnt = np.zeros(B, np.int32)
+        st = np.zeros(B, np.int32)
+
+        def one():
+            ns = ns0.copy()
+            L.or_split_batch(bufs.ctypes.data, 65535, 65535, ns.ctypes.data, oobs.ctypes.data, 24, nns.ctypes.data,
+                             n_msgs, first, B, cnt.ctypes.data, st.ctypes.data)
+            assert (cnt == ns_ * SEGS).all() and (st == 0).all()
+        return one, bps
+
+    rate, reps = _threaded_rate(make_pass, 1, seconds)
+    threads = oracle.host_threads()
+    arate, areps = _threaded_rate(make_pass, threads, seconds)
+    return {"value": round(rate / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} passes over {B} recvmmsg batches of the same shape, {seconds:.1f} s, "
+                      "C restatement of splitMessages (bytes read + written)",
+            "all_cores": {"value": round(arate / 2**30, 3), "unit": "GiB/s", "cores": threads,
+                          "host_nproc": os.cpu_count(),
+                          "sample": f"{areps} passes, one private copy of the {B} batches per thread"}}
 
 
 # ------------------------------------------------------------------ coalesce
@@ -346,6 +382,8 @@ def run_coalesce(args, torch, dev, rank, world, barrier, B=1024, max_bufs=128):
 
 
 def coalesce_cpu_baseline(pk, seconds, B=16, max_bufs=128):
+    """The oracle (C restatement of coalesceMessages) on B Send batches of the
+    same shape: 1 thread for `seconds`, then every host thread (all_cores)."""
     import ctypes as C
 
     oracle = _oracle()
@@ -353,22 +391,28 @@ def coalesce_cpu_baseline(pk, seconds, B=16, max_bufs=128):
     L.or_coalesce_batch.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
                                     C.c_int, C.c_void_p]
     L.or_coalesce_batch.restype = None
-    bufs = np.zeros((B * max_bufs, 65536), np.uint8)
-    bufs[:, :MSG] = pk[: B * max_bufs]
-    lens = np.full(B * max_bufs, MSG, np.uint64)
-    caps = np.full(B * max_bufs, 65535, np.uint64)
-    nb = np.full(B, max_bufs, np.int32)
-    nm = np.zeros(B, np.int32)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        L.or_coalesce_batch(bufs.ctypes.data, 65536, lens.ctypes.data, caps.ctypes.data, nb.ctypes.data, max_bufs, B,
-                            0, nm.ctypes.data)
-        reps += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    assert (nm == 3).all()
     bps = 2 * B * (max_bufs - 3) * MSG
-    return {"value": round(bps * reps / dt / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} passes over {B} Send batches of the same shape, {dt:.1f} s, "
-                      "C restatement of coalesceMessages (bytes read + written)"}
+
+    def make_pass():
+        bufs = np.zeros((B * max_bufs, 65536), np.uint8)
+        bufs[:, :MSG] = pk[: B * max_bufs]
+        lens = np.full(B * max_bufs, MSG, np.uint64)
+        caps = np.full(B * max_bufs, 65535, np.uint64)
+        nb = np.full(B, max_bufs, np.int32)
+        nm = np.zeros(B, np.int32)
+
+        def one():
+            L.or_coalesce_batch(bufs.ctypes.data, 65536, lens.ctypes.data, caps.ctypes.data, nb.ctypes.data, max_bufs,
+                                B, 0, nm.ctypes.data)
+            assert (nm == 3).all()
+        return one, bps
+
+    rate, reps = _threaded_rate(make_pass, 1, seconds)
+    threads = oracle.host_threads()
+    arate, areps = _threaded_rate(make_pass, threads, seconds)
+    return {"value": round(rate / 2**30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} passes over {B} Send batches of the same shape, {seconds:.1f} s, "
+                      "C restatement of coalesceMessages (bytes read + written)",
+            "all_cores": {"value": round(arate / 2**30, 3), "unit": "GiB/s", "cores": threads,
+                          "host_nproc": os.cpu_count(),
+                          "sample": f"{areps} passes, one private copy of the {B} batches per thread"}}
