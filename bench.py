@@ -338,14 +338,17 @@ def end_to_end(torch, dev, arena_np, pkts_np, mode, barrier, dist, red_dev, worl
         barrier()
         return shard.max_over_ranks((time.perf_counter() - t0) / iters, dist, device=red_dev)
 
-    dt = timed(pipelined)
+    dt_pipe = timed(pipelined)
     dt_ser = timed(serialized)
+    dt = min(dt_pipe, dt_ser)
     return {"value": round(world * nbytes / dt / 2**30, 2), "unit": "GiB/s", "ms_per_batch": round(dt * 1e3, 4),
-            "n_gpus": world, "serialized_GiB_per_s": round(world * nbytes / dt_ser / 2**30, 2),
-            "what": f"pinned H2D of the batch + kernel + D2H of the per-packet results, {len(parts)} chunks: "
-                    "H2D back to back on a copy stream, each chunk's kernel + D2H on a compute stream once it "
-                    "has landed; every rank at once (aggregate; PCIe bound). serialized_GiB_per_s: the whole "
-                    "batch H2D -> kernel -> D2H on one stream"}
+            "n_gpus": world, "strategy": "serialized" if dt_ser <= dt_pipe else "pipelined",
+            "serialized_GiB_per_s": round(world * nbytes / dt_ser / 2**30, 2),
+            "pipelined_GiB_per_s": round(world * nbytes / dt_pipe / 2**30, 2),
+            "what": "pinned H2D of the batch + kernel + D2H of the per-packet results, every rank at once "
+                    "(aggregate; PCIe bound); the faster of: serialized (whole batch H2D -> kernel -> D2H on one "
+                    f"stream) and pipelined ({len(parts)} chunks, H2D back to back on a copy stream, each chunk's "
+                    "kernel + D2H on a compute stream once it has landed)"}
 
 
 def host_call(dev, arena_np, pkts_np, mode, reps=50):

@@ -37,7 +37,7 @@ def bench_key(k):
         mode = {"2": "VALIDATE", "1": "L4_FILL"}.get(m.group(1), m.group(1))
         return f"checksum_batch_kernel<{mode},{m.group(2)},{m.group(3)},{'nt' if m.group(4) == 'true' else 'rt'}>"
     m = re.search(r"gso_rows_kernel<(\d+), (true|false)(?:, (\d+))?>", k)
-    if m:
+    if m:  # round 1 / early round 2 had a third template argument (block waves)
         return f"gso_rows_kernel<{m.group(1)},{m.group(2)}" + (f",{m.group(3)}>" if m.group(3) else ">")
     m = re.search(r"udp_split_kernel<(\d+)>", k)
     if m:

@@ -3,7 +3,7 @@
 //   wgcs_gso_split           gsoSplit()          /root/reference/tun/gro.go:1373-1493
 //   wgcs_handle_virtio_read  handleVirtioRead()  /root/reference/tun/tun.go:514-632
 // The host-buffer entry points stage the super-packet into HBM, run
-// gso_split_kernel (all validation, header rewriting, payload copies and
+// gso_rows_kernel (all validation, header rewriting, payload copies and
 // checksums happen there), and copy the produced segments back into the
 // caller's buffers.
 #include <hip/hip_runtime.h>

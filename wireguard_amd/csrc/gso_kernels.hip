@@ -6,20 +6,20 @@
 //   gsoNoneChecksum (GSO_NONE + NEEDS_CSUM) /root/reference/tun/gro.go:1497-1517
 //
 // Mapping (gso_rows_kernel): one 16-lane DPP row per OUTPUT segment (slot =
-// job * max_segs + i), 64 segments per 1024-thread block, grid = (job,
-// segment group).  Every row first issues its payload loads (dword-aligned
-// 16-byte windows, U per lane in flight, which need only gsoSize) and its
-// header-chunk loads (L2-resident, shared by the job); the decoder wave
-// meanwhile validates the job and publishes its geometry through LDS
-// (barrier 1), then computes the job-constant header sums (barrier 2) while
-// every row
+// job * max_segs + i), 16 segments per 256-thread block, grid = (job,
+// segment group).  For the common ("clean") job every wave derives the split
+// geometry from the virtio header and the header chunks it loads (one scalar
+// load + two 16-byte loads per lane), issues its payload loads (dword-aligned
+// 16-byte windows, U per lane in flight) and, with no decode step and no
+// barrier,
 //   1. shifts each window to the destination's byte phase (alignbyte with the
 //      next lane's first dword via DPP row_ror), sums the L4 bytes from the
 //      same registers (v_dot2) and stores full global_store_dwordx4 chunks;
-//   2. after barrier 2, computes the IPv4 and L4 checksums from the row sum
-//      plus the job constants and the rewritten field values, rewrites the
-//      header chunk and stores it last -- every output byte is written once.
-// The barriers order LDS only (lds_barrier): loads stay in flight across them.
+//   2. computes the IPv4 and L4 checksums from the row sum plus the header
+//      sums of its own header chunks and the rewritten field values, rewrites
+//      the header chunk and stores it last -- every output byte written once.
+// Any other job takes the decoded path: wave 0 runs the full validation and
+// publishes its verdict through LDS (one barrier), the rows follow it.
 // Reference quirks reproduced bit-for-bit: IPv4 ID is
 // id0 + 1 for every segment i >= 1; TCP seq uses a uint16 product
 // gsoSize * uint16(i); FIN/PSH cleared on all but the last segment; no UDP
@@ -42,7 +42,6 @@ enum : int { GSO_NONE = 0, GSO_TCPV4 = 1, GSO_TCPV6 = 4, GSO_UDP_L4 = 5 };
 
 __device__ __forceinline__ uint32_t u8at(const uint8_t* p) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)*p); }
 __device__ __forceinline__ uint32_t be16at(const uint8_t* p) { return (u8at(p) << 8) | u8at(p + 1); }
-__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // The first 256 bytes of a job ([virtio hdr | packet...]) held across the
 // wave, one byte per lane per register: a single batch of byte loads instead
@@ -64,16 +63,6 @@ struct HdrBytes {
     const int l = k & 63;
     const uint32_t v = k < 64 ? r0 : (k < 128 ? r1 : (k < 192 ? r2 : r3));
     return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
-  }
-  // byte k (k per lane, 0 <= k < 256) fetched across lanes (ds_bpermute, no
-  // memory access); all lanes must be active.
-  __device__ __forceinline__ uint32_t lane_byte(int k) const {
-    const int a = (k & 63) << 2;
-    const uint32_t t0 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)r0);
-    const uint32_t t1 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)r1);
-    const uint32_t t2 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)r2);
-    const uint32_t t3 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)r3);
-    return k < 64 ? t0 : (k < 128 ? t1 : (k < 192 ? t2 : t3));
   }
   __device__ __forceinline__ uint32_t le16(int k) const { return (*this)(k) | ((*this)(k + 1) << 8); }
   __device__ __forceinline__ uint32_t be16(int k) const { return ((*this)(k) << 8) | (*this)(k + 1); }
@@ -422,16 +411,6 @@ __device__ __forceinline__ void put_be16(uint4& v, int x0, int pos, uint32_t val
   put_byte(v, x0, pos + 1, val, lim);
 }
 
-template <bool NT>
-__device__ __forceinline__ uint4 ld_src(const uint8_t* p) {
-  if (NT) {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    return make_uint4(t.x, t.y, t.z, t.w);
-  }
-  return ld16(p);
-}
-
 // Job-uniform header sums for the common case ("fast" header): every
 // per-segment header write lands inside hdrLen at a position disjoint from the
 // L4 checksum field, so the per-segment IPv4 and L4 header sums are a job
@@ -505,219 +484,42 @@ __device__ __forceinline__ void put_be16_u(uint4& P, int r, int pos, uint32_t va
   }
 }
 
-// Job-level values decoded once per block by wave 0 and broadcast through LDS.
+// Job-level values decoded once per block by the decoder wave, published
+// through LDS (read by the rows before their header phase).
 struct JobInfo {
-  int32_t status, count, nseg, type, ipv, hdr_len, gso, cs, co, plen, flags, fast, gen;
+  int32_t status, count, nseg;
+  uint32_t shape;  // type | ipv << 8 | gen << 16 | fast << 24
+  int32_t hdr_len, gso, cs, co, plen, flags;
   uint32_t id0, seq0, ip_base, l4_base, addr, tflags;
 };
 
 __device__ __forceinline__ int ufl(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// Row-per-segment split.  Block = 1024 threads = 64 rows of 16 lanes = 64
-// consecutive output segments of one job; grid = (job, segment group).
-// One decoder wave decodes the job once and broadcasts it through LDS in two
-// steps (geometry, then the job-constant header sums) -- per-wave decoding
-// made the CU's shared scalar unit the bottleneck (16 decodes per CU).
-template <int U, bool NT, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void gso_rows_kernel(const uint8_t* __restrict__ arena,
-                                                        const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
-                                                        uint8_t* __restrict__ out, uint32_t out_stride,
-                                                        const GsoOutPos* __restrict__ outpos,
-                                                        uint32_t offset, uint32_t room, int32_t* __restrict__ sizes,
-                                                        int32_t* __restrict__ count, int32_t* __restrict__ status) {
-  __shared__ JobInfo ji;
-  constexpr int ROWS = 4 * WAVES;   // segments per block (one 16-lane row each)
-  __shared__ uint32_t s_tpay[ROWS];   // per segment of the block: row-reduced payload sum (dense header phase)
-  __shared__ uint4 s_keep[ROWS][8];   // per segment: payload bytes of destination chunks 0..7
-  const int lane = threadIdx.x & 63;
-  const int r = lane & 15;
-  const int wv = threadIdx.x >> 6;
-  const uint32_t jb = blockIdx.x;
-  const wgcs_gso_job job = jobs[jb];  // one scalar load of the whole descriptor, flags included
-  const uint8_t* vb = arena + job.off;
-  const uint32_t jlen = job.len;
-  const uint8_t* rb = vb + 10;
-  const uint64_t slot0 = (uint64_t)jb * max_segs;  // sizes[] index of segment 0
-  // segment i of this job at out + obase + i * opitch (+ offset): fixed slots,
-  // or the caller's packed per-job layout (the stager's compact D2H region)
-  uint64_t obase = slot0 * out_stride;
-  uint32_t opitch = out_stride;
-  if (outpos) {
-    obase = outpos[jb].base;
-    opitch = outpos[jb].pitch;
-  }
-  const uint32_t seg0 = blockIdx.y * (uint32_t)ROWS + (uint32_t)wv * 4u;  // wave-uniform
-  const int i = (int)seg0 + (lane >> 4);                       // this row's segment
-  uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
-  const int dalign = (int)((uintptr_t)dst & 15u);
-  uint8_t* dbase = dst - dalign;
-
-  // ---- decoder wave (the block's last: its rows are the least likely to
-  // exist, 45 segments per job at cfg4): validation and geometry, published
-  // through LDS at barrier 1; the job-constant header sums follow at barrier
-  // 2, computed while the other waves stream their payload.  It decodes
-  // before issuing its own speculative loads: a decode step that waited on a
-  // global load would otherwise wait (vmcnt retires in order) for that batch.
-  constexpr int kDec = WAVES - 1;
-  HdrBytes hb;
-  Job jd = {};
-  bool jd_ok = false;
-  if (wv == kDec) {
-    __builtin_amdgcn_s_setprio(3);  // the decode chain is the block's critical path (until barrier 2)
-    hb.load(vb, (int)min(jlen, 256u), lane);
-    jd = decode_job(hb, jlen, job.flags, room, max_segs);
-    jd_ok = jd.status == 0 || jd.status == WGCS_ERR_TOO_MANY_SEGMENTS;
-    if (lane == 0) {
-      ji.status = jd.status;
-      ji.count = jd_ok ? jd.count : 0;
-      ji.nseg = jd_ok ? jd.nseg : 0;
-      ji.type = jd.type;
-      ji.ipv = jd.ipv;
-      ji.hdr_len = jd.hdr_len;
-      ji.gso = jd.gso;
-      ji.cs = jd.cs;
-      ji.co = jd.co;
-      ji.plen = jd.plen;
-      ji.flags = jd.flags;
-      ji.gen = jd.gen;
-      if (blockIdx.y == 0) {
-        count[jb] = ji.count;
-        status[jb] = jd.status;
-      }
-    }
-  }
-
-  // ---- speculative first payload batch.  The source window of segment i
-  // needs only gsoSize (virtio header bytes 4-5), so every row issues its
-  // first U payload loads before the block barrier: the decode and the
-  // barrier overlap the HBM round trip instead of preceding it.  The
-  // guards keep the loads inside the job's own bytes [vb, rb + plen); bytes a
-  // window picks up outside the segment are masked exactly as on the decoded
-  // path (header positions, past pktLen).  GSO_NONE jobs skip it.
-  int gso_s = 0, type_s = GSO_NONE;
-  if (wv == kDec) {
-    if (jlen >= 10) {
-      type_s = (int)hb(1);
-      gso_s = (int)hb.le16(4);
-    }
-  } else if (jlen >= 10) {
-    type_s = (int)u8at(vb + 1);
-    gso_s = (int)(u8at(vb + 4) | (u8at(vb + 5) << 8));
-  }
-  const int plen_s = jlen >= 10 ? (int)jlen - 10 : 0;
-  const uint8_t* jend = rb + plen_s;
-  const uint8_t* w0 = rb + (int64_t)i * gso_s - dalign;  // source of destination chunk 0 (payload positions)
-  const int sb = (int)((uintptr_t)w0 & 3u);              // byte shift within dwords
-  const uint8_t* abase = w0 - sb;                        // dword-aligned window base
-  const uint4 z = make_uint4(0, 0, 0, 0);
-  uint4 A[U];
-  uint32_t E = 0;
-  // RAW jobs split whatever the type byte says (gsoSplit maps non-TCP types to
-  // UDP, gro.go:1398-1405): only handleVirtioRead's GSO_NONE copies one packet
-  const bool splits = type_s != GSO_NONE || (job.flags & WGCS_GSO_JOB_RAW) != 0;
-  const bool spec = splits && (int64_t)i * gso_s < (int64_t)plen_s;  // row-uniform
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const uint8_t* ca = abase + 16 * (r + 16 * u);
-    A[u] = (spec && ca >= vb && ca < jend) ? ld_window<NT>(ca, jend) : z;
-  }
-  if (spec && r == 15) {
-    const uint8_t* ce = abase + 16 * (16 * U);
-    if (ce >= vb && ce < jend) E = *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(ce, 4));
-  }
-
-  // ---- speculative header chunks in packet coordinates (the fast path's;
-  // bytes past hdrLen are replaced by payload bytes later): L2 hits shared by
-  // the job's segments, issued after the payload batch so waiting for the
-  // payload does not wait for them.
-  const int hph_s = (int)((uintptr_t)rb & 15u);
-  const uint8_t* hab_s = rb - hph_s + 16 * r;
-  const uint8_t* hend_s = rb + min(plen_s, kMaxHdrLen + 16);
-  // Issued unconditionally, only the address is selected (a chunk past
-  // hend_s reads the chunk holding rb, a row that does not speculate reads
-  // the job table; the fast path uses H0/H1 only when spec_ok and never their
-  // bytes past hdrLen).  Together with the decoder's raised priority: 11.74 ->
-  // 11.54 us on cfg4 (each change alone was slower, scripts/exp_gso.sh).
-  const uint8_t* hsafe = rb - hph_s;  // the 16-byte chunk holding rb
-  const uint8_t* hdummy = reinterpret_cast<const uint8_t*>(jobs);
-  uint4 H0 = ld_src<NT>(spec ? (hab_s < hend_s ? hab_s : hsafe) : hdummy);
-  uint4 H1 = ld_src<NT>(spec ? (hab_s + 16 < hend_s ? hab_s + 16 : hsafe) : hdummy);
-
-  lds_barrier();  // barrier 1: geometry; the speculative loads stay in flight
-  // block-uniform: whether the header phase (and so barrier 2) happens at all
-  const bool hdr_phase = ufl(ji.nseg) > 0 && ufl(ji.type) != GSO_NONE && ufl(ji.gen) == 0;
-  if (wv == kDec && hdr_phase) {
-    const HdrFast hf = header_fast(hb, jd, lane);
-    // readBuf bytes after gsoSplit zeroed the L4 checksum field (gro.go:1393;
-    // the IPv4 checksum bytes 10-11 are neither id nor seq here: cs >= 20)
-    const int ca = (jd.cs + jd.co) & 0xFFFF;
-    auto zb = [&](int x) { return (x == ca || x == ca + 1) ? 0u : hb(10 + x); };
-    const uint32_t id0 = jd.ipv == 4 ? (zb(4) << 8) | zb(5) : 0u;
-    const int sq = jd.cs + 4;
-    const uint32_t seq0 = jd.type != GSO_UDP_L4 ? (zb(sq) << 24) | (zb(sq + 1) << 16) | (zb(sq + 2) << 8) | zb(sq + 3) : 0u;
-    if (lane == 0) {
-      ji.fast = hf.fast ? 1 : 0;
-      ji.id0 = id0;
-      ji.seq0 = seq0;
-      ji.ip_base = hf.ip_base;
-      ji.l4_base = hf.l4_base;
-      ji.addr = hf.addr;
-      ji.tflags = hf.flags;
-    }
-    // barrier 2 (header constants).  Waves that retire early are not waited
-    // for: s_barrier only counts the workgroup's surviving waves.
-    lds_barrier();
-  }
-  if (wv == kDec) __builtin_amdgcn_s_setprio(0);
-  Job j = {};
-  j.status = ufl(ji.status);
-  j.nseg = ufl(ji.nseg);
-  j.type = ufl(ji.type);
-  if (j.nseg == 0) return;  // error status (or an empty packet)
-  j.plen = ufl(ji.plen);
-  j.cs = ufl(ji.cs);
-  j.co = ufl(ji.co);
-  j.flags = ufl(ji.flags);
-  if (j.type == GSO_NONE) {  // one packet: wave 0 of the job's first block
-    if (seg0 == 0) {
-      none_segment(rb, j, out + obase + offset, lane);
-      if (lane == 0) sizes[slot0] = j.plen;
-    }
-    return;
-  }
-  if (seg0 >= (uint32_t)j.nseg) return;
-  j.ipv = ufl(ji.ipv);
-  j.hdr_len = ufl(ji.hdr_len);
-  j.gso = ufl(ji.gso);
-  const bool v4 = j.ipv == 4, tcp = j.type != GSO_UDP_L4;
-  if (i >= j.nseg) return;  // whole rows retire; DPP below stays inside live rows
-  if (ufl(ji.gen)) {  // block-uniform: no barrier 2 for general jobs
-    gso_general_row(rb, j.plen, j.type, j.ipv, j.hdr_len, j.gso, j.cs, j.co, i, dst, r, &sizes[slot0 + (uint32_t)i]);
-    return;
-  }
-  const bool spec_ok = spec && j.gso == gso_s;  // always true: both read virtio bytes 4-5
-
-  // ---- segment geometry (row-uniform)
-  const int hdr_len = j.hdr_len, cs = j.cs, plen = j.plen;
-  const int csum_at = (cs + j.co) & 0xFFFF;
-  const int seg_start = hdr_len + i * j.gso;
-  const int seg_end = min(plen, seg_start + j.gso);
-  const int seg_len = seg_end - seg_start;
-  const int pkt_len = hdr_len + seg_len;
-  const bool last = seg_end == plen;
-  const uint64_t slot = slot0 + (uint32_t)i;
+// One row's payload stream: destination chunk k = bytes [sb, sb + 16) of the
+// dword-aligned source window k and the first dword of window k + 1 (next
+// lane, DPP row_ror).  Sums the L4 bytes [hdrLen, pktLen) from the same
+// registers (v_dot2), stores every chunk past the header chunks (k >= hk) and
+// keeps the payload part of header chunk r in `keep`.  The first batch of
+// windows may already be in A/E (loaded == true).
+template <int U, bool NT>
+__device__ __forceinline__ void stream_row(const uint8_t* rb, int i, int gso, int hdr_len, int plen, int dalign,
+                                           uint8_t* dbase, int r, uint4 (&A)[U], uint32_t& E, bool loaded,
+                                           uint32_t& acc, uint4& keep) {
+  const int seg_start = hdr_len + i * gso;
+  const int seg_end = min(plen, seg_start + gso);
+  const int pkt_len = hdr_len + (seg_end - seg_start);
   const int nk = (pkt_len + dalign + 15) >> 4;
   const int hk = min((hdr_len + dalign + 15) >> 4, nk);
   const uint8_t* src_lo = rb + seg_start;
   const uint8_t* src_hi = rb + seg_end;
-
-
-  // ---- payload stream: destination chunk k = bytes [sb, sb + 16) of the
-  // dword-aligned window k and the first dword of window k + 1 (next lane, DPP)
-  uint32_t acc = 0;  // L4 bytes [hdrLen, pktLen): LE words at destination addresses
-  uint4 keep = z;    // payload part of header chunk r (r < hk)
+  const uint8_t* w0 = rb + (int64_t)i * gso - dalign;  // source of destination chunk 0 (payload positions)
+  const int sb = (int)((uintptr_t)w0 & 3u);
+  const uint8_t* abase = w0 - sb;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  acc = 0;
+  keep = z;
   for (int k0 = 0; k0 < nk; k0 += 16 * U) {
-    if (k0 > 0 || !spec_ok) {  // wave-uniform; the first batch is normally the speculative one
+    if (k0 > 0 || !loaded) {  // wave-uniform
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint8_t* ca = abase + 16 * (k0 + r + 16 * u);
@@ -749,115 +551,302 @@ __global__ __launch_bounds__(64 * WAVES) void gso_rows_kernel(const uint8_t* __r
       }
     }
   }
+}
 
-  // ---- lane-dense header phase (fast headers of <= 113 bytes): the row
-  // publishes its payload sum and the payload part of its header chunks, and
-  // after barrier 2 Ld = 4 or 8 lanes per segment (instead of a whole 16-lane
-  // row, of which only hk lanes hold header bytes) rewrite and store the
-  // headers: 16 or 8 segments per wave, a quarter or half of the VALU issue.
-  // Block-uniform; needs the decoder wave to own no segment of this block
-  // (its rows publish only after barrier 2).
-  const int nb = min(ROWS, j.nseg - (int)(blockIdx.y * (uint32_t)ROWS));
-  const int Ld = nb <= ROWS - 4 ? (hdr_len <= 49 ? 4 : (hdr_len <= 113 ? 8 : 0)) : 0;
-  if (Ld) {
-    const uint32_t tp = fold32_16(row16_sum_u32(acc));
-    const int sloc_r = i - (int)(blockIdx.y * (uint32_t)ROWS);
-    if (r == 0) s_tpay[sloc_r] = tp;
-    if (r < 8) s_keep[sloc_r][r] = keep;
+// Byte `pos` (wave-uniform, < 16 * 16) of the header chunks in packet
+// coordinates (lane r of each row holds readBuf[16r, 16r + 16)), from the
+// wave's first row.
+__device__ __forceinline__ uint32_t qbyte(const uint4& Q, int pos) {
+  const int l = pos >> 4;
+  const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)Q.x, l), y = (uint32_t)__builtin_amdgcn_readlane((int)Q.y, l);
+  const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)Q.z, l), w = (uint32_t)__builtin_amdgcn_readlane((int)Q.w, l);
+  const int c = (pos >> 2) & 3;
+  const uint32_t d = c == 0 ? x : (c == 1 ? y : (c == 2 ? z : w));
+  return (d >> (8 * (pos & 3))) & 0xFFu;
+}
+
+// The decoded path's decoder (wave 0 of the block): handleVirtioRead's /
+// gsoSplit's checks and geometry (decode_job) and the job-constant header
+// sums (header_fast), published in `ji`; count / status of the job.  Kept out
+// of line: the rare path's registers do not count against the clean path's.
+__device__ __noinline__ void decode_publish(const uint8_t* vb, uint32_t jlen, uint32_t jflags, uint32_t room,
+                                            uint32_t max_segs, int lane, JobInfo* jip, bool first_block,
+                                            int32_t* count_j, int32_t* status_j) {
+  JobInfo& ji = *jip;
+  __builtin_amdgcn_s_setprio(3);
+  HdrBytes hb;
+  hb.load(vb, (int)min(jlen, 256u), lane);
+  const Job jd = decode_job(hb, jlen, jflags, room, max_segs);
+  const bool ok = jd.status == 0 || jd.status == WGCS_ERR_TOO_MANY_SEGMENTS;
+  uint32_t fst = 0, i0 = 0, q0 = 0;
+  HdrFast hf = {};
+  if (ok && jd.nseg > 0 && jd.type != GSO_NONE && !jd.gen) {
+    hf = header_fast(hb, jd, lane);
+    // readBuf bytes after gsoSplit zeroed the L4 checksum field (gro.go:1393;
+    // the IPv4 checksum bytes 10-11 are neither id nor seq here: cs >= 20)
+    const int ca = (jd.cs + jd.co) & 0xFFFF;
+    auto zb = [&](int x) { return (x == ca || x == ca + 1) ? 0u : hb(10 + x); };
+    const int sq = jd.cs + 4;
+    i0 = jd.ipv == 4 ? (zb(4) << 8) | zb(5) : 0u;
+    q0 = jd.type != GSO_UDP_L4 ? (zb(sq) << 24) | (zb(sq + 1) << 16) | (zb(sq + 2) << 8) | zb(sq + 3) : 0u;
+    fst = hf.fast ? 1u : 0u;
+  }
+  if (lane == 0) {
+    ji.status = jd.status;
+    ji.count = ok ? jd.count : 0;
+    ji.nseg = ok ? jd.nseg : 0;
+    ji.shape = (uint32_t)(jd.type & 0xFF) | ((uint32_t)(jd.ipv & 0xFF) << 8) |
+               ((uint32_t)(jd.gen ? 1 : 0) << 16) | (fst << 24);
+    ji.hdr_len = jd.hdr_len;
+    ji.gso = jd.gso;
+    ji.cs = jd.cs;
+    ji.co = jd.co;
+    ji.plen = jd.plen;
+    ji.flags = jd.flags;
+    ji.id0 = i0;
+    ji.seq0 = q0;
+    ji.ip_base = fold32_16(hf.ip_base);
+    ji.l4_base = fold32_16(hf.l4_base) + fold32_16(hf.addr);
+    ji.tflags = hf.flags;
+    if (first_block) {
+      *count_j = ok ? jd.count : 0;
+      *status_j = jd.status;
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// Row-per-segment split.  Block = 4 waves = 16 rows = 16 consecutive output
+// segments of one job; grid = (job, segment group).
+//
+// Clean jobs (the common case) need no decode step and no barrier.  Every
+// wave reads the virtio header (one scalar load) and derives the split
+// geometry; when that geometry takes the row-streaming path and its first
+// segment fits the caller's room, handleVirtioRead's and gsoSplit's checks
+// (tun/tun.go:557-631, gro.go:1387-1410) can fail only through the TCP data
+// offset, which the wave reads from the header chunks it loads anyway
+// (hdrLen = csumStart + dataOffset, tun.go:601-614).  Such a job's status is
+// 0 or ErrTooManySegments from the segment count alone, and each row
+// computes the header sums it needs from its own header chunks.  The row
+// streams its payload (loads issued right after the virtio header arrives),
+// then rewrites and stores its header chunks.
+//
+// Every other job (GSO_NONE, errors, unusual geometry) takes the decoded
+// path: wave 0 runs decode_job and the job-constant sums and publishes them
+// through LDS; after the barrier each row follows that verdict (nothing on an
+// error, the byte-granular general path, or the stream with the decoded
+// geometry and the general header path).
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void gso_rows_kernel(const uint8_t* __restrict__ arena,
+                                                       const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
+                                                       uint8_t* __restrict__ out, uint32_t out_stride,
+                                                       const GsoOutPos* __restrict__ outpos, uint32_t offset,
+                                                       uint32_t room, int32_t* __restrict__ sizes,
+                                                       int32_t* __restrict__ count, int32_t* __restrict__ status) {
+  constexpr int ROWS = 16;
+  __shared__ JobInfo ji;
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15;
+  const int wv = threadIdx.x >> 6;
+  const uint32_t jb = blockIdx.x;
+  const wgcs_gso_job job = jobs[jb];  // one scalar load of the whole descriptor, flags included
+  const uint8_t* vb = arena + job.off;
+  const uint32_t jlen = job.len;
+  const uint8_t* rb = vb + 10;
+  const uint64_t slot0 = (uint64_t)jb * max_segs;  // sizes[] index of segment 0
+  // segment i of this job at out + obase + i * opitch (+ offset): fixed slots,
+  // or the caller's packed per-job layout (the stager's compact D2H region)
+  uint64_t obase = slot0 * out_stride;
+  uint32_t opitch = out_stride;
+  if (outpos) {
+    obase = outpos[jb].base;
+    opitch = outpos[jb].pitch;
+  }
+  const int segb = (int)(blockIdx.y * (uint32_t)ROWS);
+  const int i = segb + wv * 4 + (lane >> 4);  // this row's segment
+  uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
+  const int dalign = (int)((uintptr_t)dst & 15u);
+  uint8_t* dbase = dst - dalign;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+
+  // ---- header chunks in packet coordinates (lane r of each row: the 16-byte
+  // aligned chunks r and r + 1 from readBuf's), issued first: they need only
+  // the descriptor, and the data-offset check below waits for them without
+  // waiting for the payload loads.  Chunks past the packet's first 256 bytes
+  // (never header bytes on the rows' path) read the chunk holding readBuf[0].
+  const int hph = (int)((uintptr_t)rb & 15u);
+  const uint8_t* hab = rb - hph + 16 * r;
+  const uint8_t* hend_s = rb + min(jlen > 10 ? (int)jlen - 10 : 0, kMaxHdrLen + 16);
+  uint4 H0 = ld16(hab < hend_s ? hab : rb - hph);
+  uint4 H1 = ld16(hab + 16 < hend_s ? hab + 16 : rb - hph);
+
+  // ---- virtio header + the IP version byte: 16 bytes from the dword below
+  // vb, one scalar load (readable: jlen >= 14 and the arena contract)
+  const bool raw = (job.flags & WGCS_GSO_JOB_RAW) != 0;
+  const int plen_s = jlen > 10 ? (int)jlen - 10 : 0;
+  uint32_t t1 = 0, hl = 0, g = 0, c = 0, o = 0, b0 = 0;
+  if (jlen >= 14) {
+    const int sh = (int)((uintptr_t)vb & 3u);
+    typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+    const u32x4a4 w = *reinterpret_cast<const u32x4a4*>(__builtin_assume_aligned(vb - sh, 4));
+    const uint64_t lo = ((uint64_t)w.y << 32) | w.x, hi = ((uint64_t)w.w << 32) | w.z;
+    // bytes [sh, sh + 11) of the 16: the virtio header and readBuf[0]
+    const uint64_t v0 = sh ? (lo >> (8 * sh)) | (hi << (64 - 8 * sh)) : lo;  // vb[0..8)
+    const uint64_t v1 = hi >> (8 * sh);                                      // vb[8..)
+    t1 = (uint32_t)(v0 >> 8) & 0xFFu;
+    hl = (uint32_t)(v0 >> 16) & 0xFFFFu;
+    g = (uint32_t)(v0 >> 32) & 0xFFFFu;
+    c = (uint32_t)(v0 >> 48) & 0xFFFFu;
+    o = (uint32_t)v1 & 0xFFFFu;
+    b0 = (uint32_t)(v1 >> 16) & 0xFFu;
+  }
+  const int type_s = raw ? ((t1 == GSO_TCPV4 || t1 == GSO_TCPV6) ? (int)t1 : GSO_UDP_L4) : (int)t1;
+  const int ipv_s = raw ? ((job.flags & WGCS_GSO_JOB_V6) ? 6 : 4) : (int)(b0 >> 4);
+  const bool tcp_s = type_s != GSO_UDP_L4;
+  const bool ok_s = jlen >= 14 && g != 0 &&
+                    (type_s == GSO_TCPV4 || type_s == GSO_TCPV6 || type_s == GSO_UDP_L4) &&
+                    ((ipv_s == 4 && type_s != GSO_TCPV6) || (ipv_s == 6 && type_s != GSO_TCPV4));
+  const int gso_s = (int)g, cs_s = (int)c, co_s = (int)o;
+  const int hdr_s = (raw || tcp_s) ? (int)hl : ((cs_s + 8) & 0xFFFF);
+  const int ca_s = (cs_s + co_s) & 0xFFFF;
+  const int pkt0_s = hdr_s + min(gso_s, plen_s - hdr_s);  // segment 0, the largest
+  const bool clean_s = ok_s && hdr_s < plen_s && cs_s >= (ipv_s == 4 ? 20 : 40) && ca_s + 2 <= hdr_s &&
+                       hdr_s <= kMaxHdrLen && (raw || !tcp_s || (hdr_s - cs_s >= 20 && hdr_s - cs_s <= 60)) &&
+                       fast_header(cs_s, hdr_s, ca_s, tcp_s) && (uint32_t)pkt0_s <= room;
+  const int nfull_s = clean_s ? (plen_s - hdr_s + gso_s - 1) / gso_s : 0;
+  const int nseg_s = min(nfull_s, (int)max_segs);
+  const bool live_s = clean_s && i < nseg_s;  // row-uniform
+
+  // ---- first payload batch (needs gsoSize only), then the header chunks in
+  // packet coordinates (L2 hits shared by the job's rows)
+  uint4 A[U];
+  uint32_t E = 0;
+  if (live_s) {
+    const uint8_t* w0 = rb + (int64_t)i * gso_s - dalign;
+    const uint8_t* abase = w0 - ((uintptr_t)w0 & 3u);
+    const uint8_t* src_lo = rb + hdr_s + i * gso_s;
+    const uint8_t* src_hi = rb + min(plen_s, hdr_s + (i + 1) * gso_s);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint8_t* ca = abase + 16 * (r + 16 * u);
+      A[u] = (ca < src_hi && ca + 16 > src_lo) ? ld_window<NT>(ca, src_hi) : z;
+    }
+    if (r == 15) {
+      const uint8_t* ce = abase + 16 * (16 * U);
+      if (ce < src_hi && ce + 4 > src_lo) E = *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(ce, 4));
+    }
+  }
+  uint4 Q = funnel(H0, H1, hph);  // readBuf[16r, 16r + 16) (bytes below hdrLen)
+  // the TCP data offset decides hdrLen (tun.go:601-614): block-uniform verdict
+  bool clean = clean_s;
+  if (clean && tcp_s && !raw) {
+    const int th = (int)((qbyte(Q, cs_s + 12) >> 4) * 4);
+    clean = ((cs_s + th) & 0xFFFF) == hdr_s;
   }
 
-  // ---- job-constant header sums (barrier 2; the decoder wave passed it already)
-  if (wv != kDec) lds_barrier();
-  const bool fast = ufl(ji.fast) != 0;
-  const uint32_t id0 = (uint32_t)ufl((int)ji.id0), seq0 = (uint32_t)ufl((int)ji.seq0);
-  const uint32_t ip_base = (uint32_t)ufl((int)ji.ip_base), l4_base = (uint32_t)ufl((int)ji.l4_base);
-  const uint32_t addr_sum = (uint32_t)ufl((int)ji.addr), tflags = (uint32_t)ufl((int)ji.tflags);
-
-  if (fast && Ld) {
-    const int spw = 64 / Ld;                   // segments per wave
-    if (wv * spw >= nb) return;                // wave-uniform: no header of this wave
-    const int sl = lane / Ld, c = lane % Ld;   // segment within the wave, header chunk
-    const int sloc = wv * spw + sl;
-    const bool valid2 = sloc < nb;             // lanes of live rows (Ld <= 16)
-    const int i2 = (int)(blockIdx.y * (uint32_t)ROWS) + (valid2 ? sloc : 0);
-    const int seg_start2 = hdr_len + i2 * j.gso;
-    const int seg_end2 = min(plen, seg_start2 + j.gso);
-    const int seg_len2 = seg_end2 - seg_start2;
-    const int pkt_len2 = hdr_len + seg_len2;
-    const bool last2 = seg_end2 == plen;
-    uint8_t* dst2 = out + obase + (uint64_t)i2 * opitch + offset;
-    const int dalign2 = (int)((uintptr_t)dst2 & 15u);
-    uint8_t* dbase2 = dst2 - dalign2;
-    const int nk2 = (pkt_len2 + dalign2 + 15) >> 4;
-    const int hk2 = min((hdr_len + dalign2 + 15) >> 4, nk2);
-    // header source chunks c, c + 1 (packet coordinates, wave-uniform phase):
-    // the speculative H0/H1 of this wave's first row, lane c (its segment
-    // speculated: it is live), fetched across lanes -- no memory round trip
-    // after the barrier.  Their bytes past hdrLen are never used.
-    const int hph = (int)((uintptr_t)rb & 15u);
-    const uint4 G0 = make_uint4((uint32_t)__shfl((int)H0.x, c), (uint32_t)__shfl((int)H0.y, c),
-                                (uint32_t)__shfl((int)H0.z, c), (uint32_t)__shfl((int)H0.w, c));
-    const uint4 G1 = make_uint4((uint32_t)__shfl((int)H1.x, c), (uint32_t)__shfl((int)H1.y, c),
-                                (uint32_t)__shfl((int)H1.z, c), (uint32_t)__shfl((int)H1.w, c));
-    const uint32_t id = i2 > 0 ? ((id0 + 1) & 0xFFFFu) : id0;  // quirk: id0 + 1 for every i >= 1 (:1426-1431)
-    const uint32_t seq = seq0 + (uint32_t)(uint16_t)((uint16_t)j.gso * (uint16_t)i2);  // uint16 product (:1445)
-    const uint32_t ulen = (uint32_t)(uint16_t)(seg_len2 + (hdr_len - cs));            // UDP length (:1462-1465)
-    const uint32_t tlen = (uint32_t)(uint16_t)(hdr_len - cs + seg_len2);              // transportLen (:1469-1471)
-    const uint32_t proto = tcp ? 6u : 17u;
-    uint32_t t_pay = s_tpay[valid2 ? sloc : 0];
-    if ((((uintptr_t)dst2 + (uintptr_t)cs) & 1u) == 0) t_pay = bswap16(t_pay);  // pairing from csumStart
-    const uint32_t var = tcp ? (seq >> 16) + (seq & 0xFFFFu) + (last2 ? (tflags & 0x09u) : 0u) : ulen;
-    const uint32_t l4c = (~fold32_16(t_pay + fold32_16(l4_base) + var + fold32_16(addr_sum) + proto + tlen)) & 0xFFFFu;
-    uint4 P = funnel(G0, G1, hph);
-    if (v4) {
-      const uint32_t ipc = (~fold32_16(fold32_16(ip_base) + (uint32_t)pkt_len2 + id)) & 0xFFFFu;
-      put_be16_u(P, c, 2, (uint32_t)pkt_len2);  // total length (:1433)
-      put_be16_u(P, c, 4, id);                  // identification (:1426-1431)
-      put_be16_u(P, c, 10, ipc);                // header checksum (:1434-1436)
-    } else {
-      put_be16_u(P, c, 4, (uint32_t)(pkt_len2 - cs));  // payload length (:1439)
+  uint32_t acc = 0;
+  uint4 keep = z;
+  int type = type_s, ipv = ipv_s, hdr_len = hdr_s, gso = gso_s, cs = cs_s, co = co_s, plen = plen_s;
+  bool fast = true;
+  uint32_t ip_base = 0, l4_base = 0, tflags = 0, id0 = 0, seq0 = 0;
+  if (clean) {
+    if (blockIdx.y == 0 && threadIdx.x == 0) {  // the checks can only end in the segment count here
+      const bool many = nfull_s > (int)max_segs;
+      count[jb] = many ? (int)max_segs - 1 : nfull_s;
+      status[jb] = many ? WGCS_ERR_TOO_MANY_SEGMENTS : 0;
     }
-    if (tcp) {
-      put_be16_u(P, c, cs + 4, seq >> 16);  // sequence number (:1445-1446)
-      put_be16_u(P, c, cs + 6, seq);
-      put_u(P, c, cs + 13, last2 ? tflags : (tflags & ~0x09u), 0xFFu);  // FIN|PSH on the last only (:1447-1459)
-    } else {
-      put_be16_u(P, c, cs + 4, ulen);
+    if (!live_s) return;
+  } else {
+    // ---- decoded path: wave 0 decodes, every wave follows its verdict
+    if (wv == 0) decode_publish(vb, jlen, job.flags, room, max_segs, lane, &ji, blockIdx.y == 0, &count[jb], &status[jb]);
+    lds_barrier();  // the decoder's verdict
+    const int st = ufl(ji.status);
+    const int nseg = ufl(ji.nseg);
+    const uint32_t shape = (uint32_t)ufl((int)ji.shape);
+    type = (int)(shape & 0xFFu);
+    if ((st != 0 && st != WGCS_ERR_TOO_MANY_SEGMENTS) || nseg == 0) return;
+    plen = ufl(ji.plen);
+    if (type == GSO_NONE) {  // one packet into bufs[0], by wave 0 of the job's first block
+      if (blockIdx.y == 0 && wv == 0) {
+        Job jn = {};
+        jn.flags = ufl(ji.flags);
+        jn.cs = ufl(ji.cs);
+        jn.co = ufl(ji.co);
+        jn.plen = plen;
+        none_segment(rb, jn, out + obase + offset, lane);
+        if (lane == 0) sizes[slot0] = plen;
+      }
+      return;
     }
-    put_be16_u(P, c, csum_at, l4c);  // L4 checksum (:1486-1490)
-    // to the destination phase: the previous chunk of the same segment (DPP
-    // row_shr:1; a group's first lane has none), merged with the payload bytes
-    uint4 Pp = row_prev4(P);
-    if (c == 0) Pp = z;
-    const uint4 D = dalign2 ? funnel_v(Pp, P, 16 - dalign2) : P;
-    const int x0h2 = 16 * c - dalign2;
-    const uint32_t hmask2 = byte_bits16(-x0h2, hdr_len - x0h2);
-    const uint4 keep2 = s_keep[valid2 ? sloc : 0][c];
-    if (valid2 && c < hk2) store_chunk(dbase2 + 16 * c, select_bytes(D, keep2, hmask2), x0h2, pkt_len2);
-    if (valid2 && c == 0) sizes[slot0 + (uint32_t)i2] = pkt_len2;
-    return;
+    if (i >= nseg) return;  // whole rows retire; DPP below stays inside live rows
+    ipv = (int)((shape >> 8) & 0xFFu);
+    fast = (shape >> 24) != 0;
+    hdr_len = ufl(ji.hdr_len);
+    gso = ufl(ji.gso);
+    cs = ufl(ji.cs);
+    co = ufl(ji.co);
+    if ((shape >> 16) & 0xFFu) {  // block-uniform
+      gso_general_row(rb, plen, type, ipv, hdr_len, gso, cs, co, i, dst, r, &sizes[slot0 + (uint32_t)i]);
+      return;
+    }
   }
-
-  // ---- header source chunks (shared by the job's segments: L2 hits).
-  // fast: packet coordinates (lane r = readBuf[16r, 16r + 16), wave-uniform
-  // phase), normally the speculative H0/H1; general: destination coordinates
-  // (per-row phase).
-  const uint8_t* hend = rb + hdr_len;
-  const int hph = fast ? (int)((uintptr_t)rb & 15u) : (int)((uintptr_t)(rb - dalign) & 15u);
-  const uint8_t* hab = (fast ? rb : rb - dalign) - hph + 16 * r;
-  if (!fast || !spec_ok) {  // row-uniform
+  // ---- the payload stream (the clean path's first batch is already in A / E)
+  stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, A, E, clean, acc, keep);
+  if (clean) {
+    // job-constant header sums from this row's own header chunks (header_fast's
+    // values): IPv4 header without total length / id / checksum, the L4
+    // header from csumStart without checksum field, seq / UDP length and the
+    // flags byte, and the pseudo-header addresses, each as BE words
+    const int x0 = 16 * r;
+    const bool tcp_c = type != GSO_UDP_L4;
+    const int vlo = cs + 4, vhi = tcp_c ? cs + 8 : cs + 6;
+    const int ca = (cs + co) & 0xFFFF;
+    if (ipv == 4) {
+      const uint32_t m = byte_bits16(-x0, cs - x0) & ~byte_bits16(2 - x0, 6 - x0) & ~byte_bits16(10 - x0, 12 - x0);
+      ip_base = (uint32_t)ufl((int)bswap16(fold32_16(row16_sum_u32(add4_masked(0u, Q, m, false)))));
+    }
+    uint32_t ml4 = byte_bits16(cs - x0, hdr_len - x0) & ~byte_bits16(ca - x0, ca + 2 - x0) &
+                   ~byte_bits16(vlo - x0, vhi - x0);
+    if (tcp_c) ml4 &= ~byte_bits16(cs + 13 - x0, cs + 14 - x0);
+    const int a_lo = ipv == 4 ? 12 : 8, a_hi = ipv == 4 ? 20 : 40;
+    uint32_t s4 = add4_masked(0u, Q, ml4, false);
+    s4 = add4_masked(s4, Q, byte_bits16(a_lo - x0, a_hi - x0), (cs & 1) != 0);
+    uint32_t t4 = fold32_16(row16_sum_u32(s4));
+    if ((cs & 1) == 0) t4 = bswap16(t4);  // pairing from csumStart (packet coordinates)
+    if (tcp_c) tflags = qbyte(Q, cs + 13);
+    l4_base = (uint32_t)ufl((int)t4) + (tflags & ~0x09u);
+    if (ipv == 4) id0 = (qbyte(Q, 4) << 8) | qbyte(Q, 5);
+    if (tcp_c) seq0 = (qbyte(Q, vlo) << 24) | (qbyte(Q, vlo + 1) << 16) | (qbyte(Q, vlo + 2) << 8) | qbyte(Q, vlo + 3);
+  } else {
+    const uint8_t* hend = rb + hdr_len;
+    const int hphd = (int)((uintptr_t)(rb - dalign) & 15u);
+    const uint8_t* hb2 = fast ? hab : rb - dalign - hphd + 16 * r;
     H0 = z;
     H1 = z;
-    if (r < hk) {
-      if (hab < hend && hab + 16 > rb) H0 = ld16(hab);
-      if (hab + 16 < hend && hab + 32 > rb) H1 = ld16(hab + 16);
-    }
+    if (hb2 < hend && hb2 + 16 > rb) H0 = ld16(hb2);
+    if (hb2 + 16 < hend && hb2 + 32 > rb) H1 = ld16(hb2 + 16);
+    Q = fast ? funnel(H0, H1, hph) : funnel_v(H0, H1, hphd);
+    ip_base = (uint32_t)ufl((int)ji.ip_base);
+    l4_base = (uint32_t)ufl((int)ji.l4_base);
+    tflags = (uint32_t)ufl((int)ji.tflags);
+    id0 = (uint32_t)ufl((int)ji.id0);
+    seq0 = (uint32_t)ufl((int)ji.seq0);
   }
 
+  // ---- segment geometry (row-uniform)
+  const bool v4 = ipv == 4, tcp = type != GSO_UDP_L4;
+  const int csum_at = (cs + co) & 0xFFFF;
+  const int seg_start = hdr_len + i * gso;
+  const int seg_end = min(plen, seg_start + gso);
+  const int seg_len = seg_end - seg_start;
+  const int pkt_len = hdr_len + seg_len;
+  const bool last = seg_end == plen;
+  const int nk = (pkt_len + dalign + 15) >> 4;
+  const int hk = min((hdr_len + dalign + 15) >> 4, nk);
   const uint32_t id = i > 0 ? ((id0 + 1) & 0xFFFFu) : id0;  // quirk: id0 + 1 for every i >= 1 (:1426-1431)
-  const uint32_t seq = seq0 + (uint32_t)(uint16_t)((uint16_t)j.gso * (uint16_t)i);  // uint16 product (:1445)
-  const uint32_t ulen = (uint32_t)(uint16_t)(seg_len + (hdr_len - cs));            // UDP length (:1462-1465)
-  const uint32_t tlen = (uint32_t)(uint16_t)(hdr_len - cs + seg_len);              // transportLen (:1469-1471)
+  const uint32_t seq = seq0 + (uint32_t)(uint16_t)((uint16_t)gso * (uint16_t)i);  // uint16 product (:1445)
+  const uint32_t ulen = (uint32_t)(uint16_t)(seg_len + (hdr_len - cs));           // UDP length (:1462-1465)
+  const uint32_t tlen = (uint32_t)(uint16_t)(hdr_len - cs + seg_len);             // transportLen (:1469-1471)
   const uint32_t proto = tcp ? 6u : 17u;
   const int x0h = 16 * r - dalign;
   const uint32_t hmask = byte_bits16(-x0h, hdr_len - x0h);  // header positions of destination chunk r
@@ -867,11 +856,11 @@ __global__ __launch_bounds__(64 * WAVES) void gso_rows_kernel(const uint8_t* __r
     uint32_t t_pay = fold32_16(row16_sum_u32(acc));
     if ((((uintptr_t)dst + (uintptr_t)cs) & 1u) == 0) t_pay = bswap16(t_pay);  // pairing from csumStart
     const uint32_t var = tcp ? (seq >> 16) + (seq & 0xFFFFu) + (last ? (tflags & 0x09u) : 0u) : ulen;
-    const uint32_t l4c = (~fold32_16(t_pay + fold32_16(l4_base) + var + fold32_16(addr_sum) + proto + tlen)) & 0xFFFFu;
+    const uint32_t l4c = (~fold32_16(t_pay + l4_base + var + proto + tlen)) & 0xFFFFu;
     // ---- header chunk in packet coordinates, rewritten (gro.go:1418-1465, :1486-1490)
-    uint4 P = funnel(H0, H1, hph);
+    uint4 P = Q;
     if (v4) {
-      const uint32_t ipc = (~fold32_16(fold32_16(ip_base) + (uint32_t)pkt_len + id)) & 0xFFFFu;
+      const uint32_t ipc = (~fold32_16(ip_base + (uint32_t)pkt_len + id)) & 0xFFFFu;
       put_be16_u(P, r, 2, (uint32_t)pkt_len);  // total length (:1433)
       put_be16_u(P, r, 4, id);                 // identification (:1426-1431)
       put_be16_u(P, r, 10, ipc);               // header checksum (:1434-1436)
@@ -886,18 +875,19 @@ __global__ __launch_bounds__(64 * WAVES) void gso_rows_kernel(const uint8_t* __r
       put_be16_u(P, r, cs + 4, ulen);
     }
     put_be16_u(P, r, csum_at, l4c);  // L4 checksum (:1486-1490)
-    // ---- to destination phase, merge with the payload bytes, store
+    // ---- to the destination phase (previous chunk of the row: DPP row_shr:1),
+    // merged with the payload bytes, stored
     const uint4 Pp = row_prev4(P);
     const uint4 D = dalign ? funnel_v(Pp, P, 16 - dalign) : P;
     if (r < hk) store_chunk(dbase + 16 * r, select_bytes(D, keep, hmask), x0h, pkt_len);
   } else {
-    // ---- general header path (unusual csum offsets / short RAW headers):
-    // byte-exact replay of the reference's write order on the chunk
+    // ---- general header path (unusual csum offsets): byte-exact replay of
+    // the reference's write order on the chunk (destination coordinates)
     const int a_lo = v4 ? 12 : 8, a_hi = v4 ? 20 : 40;
     uint32_t acc_ip = 0;
     uint4 hv = z;
     if (r < hk) {
-      hv = select_bytes(funnel_v(H0, H1, hph), keep, hmask);
+      hv = select_bytes(Q, keep, hmask);
       // readBuf's zeroed fields (gro.go:1388,:1393), then the per-segment header writes in order
       if (v4) put_be16(hv, x0h, 10, 0, hdr_len);
       put_be16(hv, x0h, csum_at, 0, hdr_len);
@@ -930,7 +920,7 @@ __global__ __launch_bounds__(64 * WAVES) void gso_rows_kernel(const uint8_t* __r
       store_chunk(dbase + 16 * r, hv, x0h, pkt_len);
     }
   }
-  if (r == 0) sizes[slot] = pkt_len;
+  if (r == 0) sizes[slot0 + (uint32_t)i] = pkt_len;
 }
 
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs, uint8_t* out,
@@ -939,14 +929,10 @@ hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs
                                   uint32_t room) {
   if (n_jobs == 0 || max_segs == 0) return hipSuccess;
   if (!outpos) room = out_stride > offset ? out_stride - offset : 0;
-  // 16 waves = 64 segments per 1024-thread block.  Smaller blocks (8 / 4 waves,
-  // more decodes per CU) measured slower on cfg4: 12.7 / 13.0 vs 11.6 us.
-  constexpr int kWaves = 16;
-  const uint32_t rows = 4u * (uint32_t)kWaves;
-  const uint32_t gy = (max_segs + rows - 1) / rows;
+  const uint32_t gy = (max_segs + 15) / 16;  // 16 segments (4 waves) per block
   if (gy > 65535u) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gso_rows_kernel<6, true, kWaves>), dim3(n_jobs, gy), dim3(64 * kWaves), 0, s, arena, jobs,
-                     max_segs, out, out_stride, outpos, offset, room, sizes, count, status);
+  hipLaunchKernelGGL((gso_rows_kernel<6, true>), dim3(n_jobs, gy), dim3(256), 0, s, arena, jobs, max_segs, out,
+                     out_stride, outpos, offset, room, sizes, count, status);
   return hipGetLastError();
 }
 
