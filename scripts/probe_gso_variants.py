@@ -5,6 +5,8 @@ Each variant is the library built with timing-only -D switches that existed
 only in the experimental revisions of gso_kernels.hip this script was run
 against (wrong output by design, except `base`; the switches were removed
 with the experiment, the outputs are kept in profiles/r2_probe_gso_*.jsonl):
+  WGCS_P_NTST        non-temporal payload stores
+  WGCS_P_U=n         n payload windows per lane in flight (default 6)
   WGCS_P_NODEC       the decoder wave publishes the rows' own geometry instead
                      of decoding (no validation, zero header constants)
   WGCS_P_CONSTJOB    the rows take cfg4's job descriptor and virtio header as
@@ -28,10 +30,10 @@ sys.path.insert(0, ROOT)
 OUTDIR = os.path.join(ROOT, "scripts", "probe_so")
 VARIANTS = {
     "base": [],
-    "nodec": ["WGCS_P_NODEC"],
-    "nodec_constjob": ["WGCS_P_NODEC", "WGCS_P_CONSTJOB"],
-    "nobar_constjob": ["WGCS_P_NOBAR", "WGCS_P_CONSTJOB"],
-    "nobar": ["WGCS_P_NOBAR"],
+    "ntst": ["WGCS_P_NTST"],
+    "u4": ["WGCS_P_U=4"],
+    "u8": ["WGCS_P_U=8"],
+    "u3": ["WGCS_P_U=3"],
 }
 
 
