@@ -52,6 +52,11 @@ if want prof; then
   (cd /tmp && step prof_cfg2 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg2" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e)
   (cd /tmp && step prof_cfg2_1s 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg2_1s" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e --streams 1)
   (cd /tmp && step prof_cfg4 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg4" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 100 --warmup 10 --cpu-seconds 0 --no-e2e)
+  (cd /tmp && step prof_cfg4_1s 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg4_1s" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 100 --warmup 10 --cpu-seconds 0 --no-e2e --streams 1)
+  for d in prof_cfg2 prof_cfg2_1s prof_cfg4 prof_cfg4_1s; do
+    k=checksum_batch; case $d in prof_cfg4*) k=gso_rows;; esac
+    python3 scripts/trace_span.py "$OUT/$d/run_kernel_trace.csv" $k 50 20 | sed "s/^{/{\"run\": \"$d\", /" >> "$OUT/trace_span.jsonl"
+  done
 fi
 if want pmc; then
   (cd /tmp && step pmcf_cfg2 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_cfg2" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 30 --warmup 3 --cpu-seconds 0 --no-e2e --no-event-timing --streams 1)
