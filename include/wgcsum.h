@@ -22,6 +22,7 @@
  *   wgcs_handle_virtio_read   handleVirtioRead(readBuf, bufs, sizes, offset)  tun/tun.go:514-632
  *   wgcs_handle_gro           handleGRO(bufs, offset, tcpTable, udpTable, canUDPGRO, &toWrite)
  *                                                                 tun/gro.go:1326-1367
+ *   wgcs_handle_gro_batch     device-resident batch of handleGRO calls (one per Tun.Write)
  *   wgcs_get_gso_size         getGSOSize(control)                 conn/gso.go:35-67
  *   wgcs_set_gso_size         setGSOSize(&control, gsoSize)       conn/gso.go:71-100
  *   wgcs_split_messages       splitMessages(msgs, firstMsgAt)     conn/bind.go:542-597
@@ -185,6 +186,37 @@ int wgcs_handle_virtio_read(wgcs_ctx *ctx, uint8_t *read_buf, size_t n, uint8_t 
  * entries, gro.go:696-697); to_write receives the indices to write. */
 int wgcs_handle_gro(wgcs_ctx *ctx, uint8_t **bufs, size_t *lens, size_t *caps, int n,
                     int offset, int can_udp_gro, int *to_write, int *n_to_write);
+
+/* ---- device-resident batch of Tun.Write calls (handleGRO per call) ----
+ * bufs[i] of a call is the Go slice d_arena[off : off+len] with cap(bufs[i]) =
+ * cap; every slice owns d_arena[off, off+cap), and the arena must be readable
+ * through align_up(off+cap, 16).  Call c runs handleGRO(bufs[first :
+ * first+n], offset, ..., canUDPGRO = flags & WGCS_GRO_CAN_UDP) on the device,
+ * in place, as the reference mutates its slices: the slice headers in d_bufs
+ * after the prepend swaps and appends (gro.go:685-697), d_status[c] = 0,
+ * WGCS_ERR_INVALID_OFFSET (gro.go:1335-1337: the earlier buffers keep what the
+ * coalescing wrote, nothing is applied, d_n_write[c] = 0) or
+ * WGCS_ERR_INVALID_ARG (n > WGCS_GRO_MAX_CALL or offset < 0: nothing touched),
+ * and toWrite in d_to_write[first : first + d_n_write[c]].  Every byte that
+ * Tun.Write hands to write(2) -- bufs[i][offset-10:len] for i in toWrite --
+ * equals the reference's, and so does every other byte of every slice.
+ * One workgroup per call, async on stream. */
+typedef struct wgcs_gro_buf {
+  uint64_t off; /* slice start in the arena */
+  uint32_t len; /* len(bufs[i]) (offset + packet length) */
+  uint32_t cap; /* cap(bufs[i]) */
+} wgcs_gro_buf;
+typedef struct wgcs_gro_call {
+  uint32_t first; /* index of bufs[0] in d_bufs (and of toWrite[0] in d_to_write) */
+  uint32_t n;     /* len(bufs) */
+  int32_t offset; /* Tun.Write's offset */
+  uint32_t flags; /* WGCS_GRO_CAN_UDP */
+} wgcs_gro_call;
+#define WGCS_GRO_CAN_UDP 0x1u
+#define WGCS_GRO_MAX_CALL 256
+int wgcs_handle_gro_batch(wgcs_ctx *ctx, uint8_t *d_arena, wgcs_gro_buf *d_bufs, const wgcs_gro_call *d_calls,
+                          uint32_t n_calls, int32_t *d_status, int32_t *d_n_write, int32_t *d_to_write,
+                          void *stream);
 
 /* ---- Tun.Read batch staging (tun/tun.go:477-508) ----
  * A ring of `depth` batches.  Each batch stages up to max_reads TUN reads

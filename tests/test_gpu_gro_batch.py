@@ -1,0 +1,134 @@
+"""GPU parity: the device-resident batch of Tun.Write calls
+(wgcs_handle_gro_batch, one workgroup per call) vs the oracle's handleGRO per
+call -- status, toWrite, the slice headers after the prepend swaps and
+appends, and every byte of every buffer (tun/tun.go:654-700,
+gro.go:1326-1367).  The calls are the write-stager cases (mixed TCP/UDP,
+v4/v6, PSH, prepends, capacity limits, UDP GRO off, invalid offsets, bad
+checksums) plus one call per edge case."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from wireguard_amd.tun import GRO_BUF_DTYPE, GRO_CALL_DTYPE, GRO_CAN_UDP
+
+from test_gpu_gro import flow
+from test_gpu_wstager import OFFSET, _calls, _mk
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(dev, calls):
+    """calls: [(pkts, cap, can_udp, lens_override)] -> per call (status,
+    to_write, bufs_out) and the final arena, next to the oracle's buffers."""
+    host_bufs, lens_all, meta = [], [], []
+    for pkts, cap, can_udp, lo in calls:
+        bufs, lens = _mk(pkts, cap, OFFSET, lo)
+        meta.append((len(host_bufs), len(bufs), can_udp))
+        host_bufs += bufs
+        lens_all += lens
+    offs, pos = [], 0
+    for b in host_bufs:
+        offs.append(pos)
+        pos += (len(b) + 15) // 16 * 16 + 16
+    arena = np.zeros(pos + 64, np.uint8)
+    for o, b in zip(offs, host_bufs):
+        arena[o: o + len(b)] = b
+    gb = np.zeros(len(host_bufs), GRO_BUF_DTYPE)
+    gb["off"] = offs
+    gb["len"] = lens_all
+    gb["cap"] = [len(b) for b in host_bufs]
+    gc = np.zeros(len(calls), GRO_CALL_DTYPE)
+    for c, (first, n, can_udp) in enumerate(meta):
+        gc[c] = (first, n, OFFSET, GRO_CAN_UDP if can_udp else 0)
+    d_arena = torch.from_numpy(arena).cuda()
+    d_bufs = torch.from_numpy(gb.view(np.uint8)).cuda()
+    d_calls = torch.from_numpy(gc.view(np.uint8)).cuda()
+    st = torch.zeros(len(calls), dtype=torch.int32, device="cuda")
+    nw = torch.zeros(len(calls), dtype=torch.int32, device="cuda")
+    tw = torch.full((len(host_bufs),), -7, dtype=torch.int32, device="cuda")
+    dev.handle_gro_batch(d_arena, d_bufs, d_calls, len(calls), st, nw, tw)
+    torch.cuda.synchronize()
+    return (meta, offs, host_bufs, lens_all, arena, d_arena.cpu().numpy(), d_bufs.cpu().numpy().view(GRO_BUF_DTYPE),
+            st.cpu().numpy(), nw.cpu().numpy(), tw.cpu().numpy())
+
+
+def _check(dev, calls):
+    meta, offs, host_bufs, lens_all, arena0, arena, gb, st, nw, tw = _run(dev, calls)
+    compared = 0
+    for c, (first, n, can_udp) in enumerate(meta):
+        bo = [host_bufs[first + i].copy() for i in range(n)]
+        lo = lens_all[first: first + n]
+        rc, tw_o, order, nl = oracle.handle_gro(bo, list(lo), OFFSET, can_udp)
+        assert st[c] == rc, (c, st[c], rc)
+        if rc == 0:
+            assert nw[c] == len(tw_o), c
+            assert list(tw[first: first + nw[c]]) == list(tw_o), c
+        for i in range(n):  # slice headers: buffer at position i and its length
+            g = gb[first + i]
+            assert g["off"] == offs[first + order[i]], (c, i)
+            assert g["len"] == nl[i], (c, i, g["len"], nl[i])
+        for j in range(n):  # every byte of every buffer, by buffer identity
+            o = offs[first + j]
+            got = arena[o: o + len(bo[j])]
+            if not np.array_equal(got, bo[j]):
+                diff = np.flatnonzero(got != bo[j])
+                bad = int(diff[0])
+                pos = order.index(j)
+                raise AssertionError(
+                    f"call {c} buffer {j} (now at position {pos}, len {lo[j]} -> {nl[pos]}, cap {len(bo[j])}, "
+                    f"to_write {pos in tw_o}, {len(diff)} bytes differ in [{bad}, {int(diff[-1])}]): "
+                    f"got {got[bad:bad + 8].tobytes().hex()} want {bo[j][bad:bad + 8].tobytes().hex()} "
+                    f"orig {host_bufs[first + j][bad:bad + 8].tobytes().hex()}; lens {lo[:12]}")
+        compared += 1
+    return compared
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_gro_batch_matches_handle_gro(dev, seed):
+    calls = _calls(seed)
+    assert _check(dev, calls) == len(calls)
+
+
+def test_gro_batch_edge_calls(dev):
+    f4 = flow(8, seg=1448, seed=7)
+    f6 = flow(8, seg=1000, v6=True, seed=8)
+    u4 = flow(8, seg=1200, udp=True, seed=9)
+    rev = list(reversed(f4))  # a prepend chain
+    calls = [
+        (f4, 65535, True, None),
+        (rev, 65535, True, None),
+        (f4 + f6 + u4, 65535, True, None),
+        (u4, 65535, False, None),                       # UDP GRO off: every packet written as-is
+        (f4[:1], 65535, True, None),                    # one packet
+        (f4, lambda n: OFFSET + n, True, None),         # no spare capacity: nothing merges
+        (f4, 65535, True, {0: OFFSET}),                 # invalid offset on the first buffer
+        (f4 + u4, 65535, True, {5: 3}),                 # invalid offset part-way (len < offset)
+        ([bytes(40)] * 4 + f4, 65535, True, None),      # non-candidates first
+    ]
+    assert _check(dev, calls) == len(calls)
+
+
+def test_gro_batch_bad_checksums_and_flags(dev):
+    rng = np.random.default_rng(5)
+    calls = []
+    for k in range(12):
+        fs = [flow(int(rng.integers(2, 10)), seg=int(rng.choice([536, 1448])), v6=bool(k & 1), udp=bool(k & 2),
+                   seed=100 + 10 * k + j, last_flags=int(rng.choice([0x10, 0x18]))) for j in range(3)]
+        pk = [p for f in fs for p in f]
+        for _ in range(int(rng.integers(0, 4))):
+            i = int(rng.integers(0, len(pk)))
+            b = bytearray(pk[i])
+            b[int(rng.integers(20, len(b)))] ^= 0x41
+            pk[i] = bytes(b)
+        order = np.argsort(rng.random(len(pk)) + np.arange(len(pk)) * 0.05)
+        calls.append(([pk[i] for i in order], 65535, True, None))
+    assert _check(dev, calls) == len(calls)
+
+
+def test_gro_batch_rejects_oversized_call(dev):
+    f = flow(4, seed=11)
+    calls = [(f * 65, 65535, True, None)]  # 260 buffers > WGCS_GRO_MAX_CALL
+    meta, offs, host_bufs, lens_all, arena0, arena, gb, st, nw, tw = _run(dev, calls)
+    assert st[0] == -1 and nw[0] == 0  # WGCS_ERR_INVALID_ARG, nothing touched
+    assert np.array_equal(arena, arena0)

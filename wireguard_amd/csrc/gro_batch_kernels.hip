@@ -1,0 +1,588 @@
+// gro_batch_kernels.hip -- gfx950 device-resident batched handleGRO: many
+// Tun.Write calls (/root/reference/tun/tun.go:654-700) whose packets are
+// already in HBM, one workgroup per call, everything on the GPU.
+//
+// handleGRO (gro.go:1326-1367) is order-dependent inside one call (flow
+// table, sequence adjacency, prepend swaps) but calls are independent, so the
+// batch maps to one 256-thread block per call:
+//   1. every thread takes one buffer: slice header, handleGRO's offset check,
+//      groCandidate (gro.go:1280-1317), the tcpGRO / udpGRO pre-checks that end
+//      in groResultNoop, and the header fields the table needs (seq, gsoSize,
+//      PSH, the IP fields ipHeadersCanCoalesce compares);
+//   2. flow ids: each packet finds the first earlier packet of its table with
+//      the same flow key (tcpFlowKey / udpFlowKey, gro.go:96-127, :252-275);
+//      checksumValid (gro.go:554-612) of every candidate, one 16-lane DPP row
+//      per packet -- exact up front because the reference validates before it
+//      mutates (gro.go:665-681, :709-723, :767-775);
+//   3. thread 0 replays the loop of handleGRO over those precomputed fields:
+//      tcpGRO / udpGRO with the flow table as per-flow linked lists of items
+//      in LDS, coalesceTCPPackets / coalesceUDPPackets as piece lists (no byte
+//      moves yet), the prepend swaps of bufs, toWrite;
+//   4. every wave applies it in place, one buffer each: the pieces the
+//      reference appended behind the buffer's own packet (copied from the
+//      original packet bytes), then applyTCPCoalesce / applyUDPCoalesce's
+//      header rewrite and virtio header (gro.go:1099-1268); a buffer that a
+//      prepend moved out of its item gets the appends it had received; then
+//      the slice headers.
+// Reads of step 4 never overlap its writes: pieces are read from packet bytes
+// below a buffer's original length (never written: only item heads' headers
+// and bytes past a buffer's original length are), in the buffer's own region.
+#include <hip/hip_runtime.h>
+
+#include "../../include/wgcsum.h"
+#include "wgcs_common.h"
+#include "wgcs_copy.h"
+#include "wgcs_kernels.h"
+
+namespace wgcs {
+
+namespace {
+
+constexpr int kMaxB = WGCS_GRO_MAX_CALL;  // buffers per call (one per thread)
+constexpr int kNone = -1;
+constexpr int kVnet = 10;
+enum : uint8_t { C_NOT = 0, C_TCP4 = 1, C_TCP6 = 2, C_UDP4 = 3, C_UDP6 = 4 };
+enum { R_NOOP = 0, R_INSERT = 1, R_COALESCED = 2 };
+enum { CC_PREPEND = -1, CC_UNAV = 0, CC_APPEND = 1 };
+enum { CR_INSUFF = 0, CR_PSH = 1, CR_ITEM_BAD = 2, CR_PKT_BAD = 3, CR_OK = 4 };
+
+struct GroSmem {
+  uint64_t boff[kMaxB];                 // arena offset of each original buffer
+  uint32_t blen[kMaxB], bcap[kMaxB];    // its slice length / capacity
+  uint32_t seq[kMaxB], ipattr[kMaxB], keyh[kMaxB], opth[kMaxB];
+  uint32_t slen[kMaxB];                 // len(bufs[s]) of the slice now at position s
+  uint32_t it_seq[kMaxB];
+  uint32_t m_pos[2 * kMaxB];            // materializations: first byte of the pieces in the buffer
+  uint16_t gso[kMaxB], flow[kMaxB], pstart[kMaxB], plen[kMaxB], it_nm[kMaxB], it_gso[kMaxB];
+  int16_t pnext[kMaxB], sbuf[kMaxB], shead[kMaxB], stail[kMaxB];
+  int16_t it_slot[kMaxB], it_prev[kMaxB], it_next[kMaxB], fl_head[kMaxB], fl_tail[kMaxB];
+  int16_t to_write[kMaxB], scount[kMaxB];
+  int16_t m_buf[2 * kMaxB], m_first[2 * kMaxB], m_count[2 * kMaxB], m_item[2 * kMaxB];  // m_item: -1 = plain
+  uint8_t m_psh[2 * kMaxB];
+  uint8_t cand[kMaxB], noop[kMaxB], iph[kMaxB], th[kMaxB], psh[kMaxB], valid[kMaxB], spsh[kMaxB], szero[kMaxB];
+  uint8_t it_iph[kMaxB], it_l4h[kMaxB], it_psh[kMaxB], it_bad[kMaxB], it_alive[kMaxB], it_cand[kMaxB];
+  int n_eff, n_items, n_write, n_mat;
+};
+
+__device__ __forceinline__ uint32_t be16g(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+__device__ __forceinline__ uint32_t be32g(const uint8_t* p) { return (be16g(p) << 16) | be16g(p + 2); }
+
+__device__ __forceinline__ uint32_t fnv(uint32_t h, uint32_t b) { return (h ^ b) * 16777619u; }
+
+// ---- thread 0: the handleGRO loop over the precomputed fields --------------
+
+struct Planner {
+  GroSmem& S;
+  const uint8_t* arena;
+  int offset;
+
+  __device__ const uint8_t* pkt(int p) const { return arena + S.boff[p] + offset; }
+  __device__ int plen_slot(int s) const { return (int)S.slen[s] - offset; }
+
+  __device__ void insert(int bi, int f, uint8_t bad) {  // tcpGROTable.insert / udpGROTable.insert
+    const int it = S.n_items++;
+    S.it_slot[it] = (int16_t)bi;
+    S.it_seq[it] = S.seq[bi];
+    S.it_nm[it] = 0;
+    S.it_gso[it] = S.gso[bi];
+    S.it_iph[it] = S.iph[bi];
+    S.it_l4h[it] = S.cand[bi] <= C_TCP6 ? S.th[bi] : 8;
+    S.it_psh[it] = S.psh[bi];
+    S.it_bad[it] = bad;
+    S.it_alive[it] = 1;
+    S.it_cand[it] = S.cand[bi];
+    S.it_next[it] = kNone;
+    S.it_prev[it] = S.fl_tail[f];
+    if (S.fl_tail[f] != kNone) S.it_next[S.fl_tail[f]] = (int16_t)it;
+    else S.fl_head[f] = (int16_t)it;
+    S.fl_tail[f] = (int16_t)it;
+  }
+
+  // A buffer's bytes as the reference leaves them: its own packet (in place)
+  // followed by `count` pieces starting at node `first`; item >= 0: also the
+  // apply* header rewrite and virtio header of that item.
+  __device__ void materialize(int buf, int first, int count, uint32_t pos, uint8_t pshf, int item) {
+    const int k = S.n_mat++;
+    S.m_buf[k] = (int16_t)buf;
+    S.m_first[k] = (int16_t)first;
+    S.m_count[k] = (int16_t)count;
+    S.m_pos[k] = pos;
+    S.m_psh[k] = pshf;
+    S.m_item[k] = (int16_t)item;
+  }
+
+  __device__ void unlink(int it, int f) {  // tcpGROTable.deleteAt (gro.go:241-247)
+    const int p = S.it_prev[it], n = S.it_next[it];
+    if (p != kNone) S.it_next[p] = (int16_t)n;
+    else S.fl_head[f] = (int16_t)n;
+    if (n != kNone) S.it_prev[n] = (int16_t)p;
+    else S.fl_tail[f] = (int16_t)p;
+    S.it_alive[it] = 0;
+  }
+
+  __device__ bool options_equal(int bi, int tgt, int tgt_iph) const {  // gro.go:442-448
+    const int n = S.th[bi] - 20;
+    if (S.opth[bi] != S.opth[tgt]) return false;
+    const uint8_t* a = pkt(bi) + S.iph[bi] + 20;
+    const uint8_t* b = pkt(tgt) + tgt_iph + 20;
+    for (int k = 0; k < n; ++k)
+      if (a[k] != b[k]) return false;
+    return true;
+  }
+
+  // tcpPacketsCanCoalesce (gro.go:433-512)
+  __device__ int tcp_can(int bi, int it) const {
+    const int s = S.it_slot[it];
+    const int tgt = S.shead[s];  // the buffer's head packet: its header
+    if (S.th[bi] != S.it_l4h[it]) return CC_UNAV;
+    if (S.th[bi] > 20 && !options_equal(bi, tgt, S.it_iph[it])) return CC_UNAV;
+    if (S.ipattr[bi] != S.ipattr[tgt]) return CC_UNAV;  // ipHeadersCanCoalesce (gro.go:392-427)
+    const uint32_t g = S.it_gso[it];
+    const uint16_t lhs = (uint16_t)(g + (uint16_t)(g * S.it_nm[it]));
+    if (S.seq[bi] == S.it_seq[it] + (uint32_t)lhs) {
+      if (S.it_psh[it]) return CC_UNAV;
+      if ((plen_slot(s) - (S.iph[bi] + S.th[bi])) % (int)g != 0) return CC_UNAV;
+      if (S.gso[bi] > g) return CC_UNAV;
+      return CC_APPEND;
+    }
+    if (S.seq[bi] + S.gso[bi] == S.it_seq[it]) {
+      if (S.psh[bi]) return CC_UNAV;
+      if (S.gso[bi] < g) return CC_UNAV;
+      if (S.gso[bi] > g && S.it_nm[it] > 0) return CC_UNAV;
+      return CC_PREPEND;
+    }
+    return CC_UNAV;
+  }
+
+  // coalesceTCPPackets (gro.go:630-741): appends become pieces
+  __device__ int tcp_coalesce(int mode, int bi, int it) {
+    const int s = S.it_slot[it];
+    const int pl = plen_slot(bi);
+    const int hdrs = (uint8_t)(S.it_iph[it] + S.it_l4h[it]);
+    const int pay = pl - hdrs;
+    const int new_len = plen_slot(s) + pay;
+    if (mode == CC_PREPEND) {
+      if ((int)S.bcap[S.sbuf[bi]] - offset < new_len) return CR_INSUFF;
+      if (S.psh[bi]) return CR_PSH;
+      if (S.it_nm[it] == 0 && !S.valid[s]) return CR_ITEM_BAD;
+      if (!S.valid[bi]) return CR_PKT_BAD;
+      S.it_seq[it] = S.seq[bi];
+      const int item_pay = new_len - pl;
+      const int h0 = S.shead[s];  // the item's head loses its headers (gro.go:690-693)
+      // the item's buffer leaves the table holding what the appends wrote into
+      // it (and the PSH they set): it keeps those bytes (gro.go:696-697)
+      if (S.scount[s] > 1 || S.spsh[s])
+        materialize(S.sbuf[s], S.pnext[h0], S.scount[s] - 1, S.plen[h0], S.spsh[s], kNone);
+      S.pstart[h0] = (uint16_t)(S.pstart[h0] + hdrs);
+      S.plen[h0] = (uint16_t)(S.plen[h0] - hdrs);
+      S.pnext[S.stail[bi]] = (int16_t)h0;
+      S.stail[bi] = S.stail[s];
+      S.slen[bi] += (uint32_t)item_pay;
+      S.scount[bi] = (int16_t)(S.scount[bi] + S.scount[s]);
+      // bufs[item.bufsIndex], bufs[pktBuffsIndex] = ... (gro.go:696-697)
+      int16_t t16;
+      uint32_t t32;
+      uint8_t t8;
+      t16 = S.sbuf[s]; S.sbuf[s] = S.sbuf[bi]; S.sbuf[bi] = t16;
+      t32 = S.slen[s]; S.slen[s] = S.slen[bi]; S.slen[bi] = t32;
+      t16 = S.shead[s]; S.shead[s] = S.shead[bi]; S.shead[bi] = t16;
+      t16 = S.stail[s]; S.stail[s] = S.stail[bi]; S.stail[bi] = t16;
+      t8 = S.spsh[s]; S.spsh[s] = S.spsh[bi]; S.spsh[bi] = t8;
+      t16 = S.scount[s]; S.scount[s] = S.scount[bi]; S.scount[bi] = t16;
+    } else {
+      if ((int)S.bcap[S.sbuf[s]] - offset < new_len) return CR_INSUFF;
+      if (S.it_nm[it] == 0 && !S.valid[s]) return CR_ITEM_BAD;
+      if (!S.valid[bi]) return CR_PKT_BAD;
+      if (S.psh[bi]) {  // pktHead[iphLen+13] |= PSH (gro.go:724-729)
+        S.it_psh[it] = 1;
+        S.spsh[s] = 1;
+      }
+      S.pstart[bi] = (uint16_t)hdrs;
+      S.plen[bi] = (uint16_t)pay;
+      S.pnext[bi] = kNone;
+      S.pnext[S.stail[s]] = (int16_t)bi;
+      S.stail[s] = (int16_t)bi;
+      S.scount[s]++;
+      S.slen[s] += (uint32_t)pay;
+    }
+    if (S.gso[bi] > S.it_gso[it]) S.it_gso[it] = S.gso[bi];
+    S.it_nm[it]++;
+    return CR_OK;
+  }
+
+  // tcpGRO (gro.go:801-963) after its pre-checks (step 1)
+  __device__ int tcp_gro(int bi) {
+    const int f = S.flow[bi];
+    int it = S.fl_tail[f];
+    while (it != kNone) {  // items of the flow, last to first
+      const int prev = S.it_prev[it];
+      const int can = tcp_can(bi, it);
+      if (can != CC_UNAV) {
+        const int r = tcp_coalesce(can, bi, it);
+        if (r == CR_OK) return R_COALESCED;
+        if (r == CR_ITEM_BAD) unlink(it, f);  // deleteAt
+        else if (r == CR_PKT_BAD) return R_NOOP;
+      }
+      it = prev;
+    }
+    insert(bi, f, 0);
+    return R_INSERT;
+  }
+
+  // udpGRO (gro.go:971-1095) after its pre-checks
+  __device__ int udp_gro(int bi) {
+    const int f = S.flow[bi];
+    const int it = S.fl_tail[f];
+    if (it == kNone) {
+      insert(bi, f, 0);
+      return R_INSERT;
+    }
+    const int s = S.it_slot[it];
+    const int tgt = S.shead[s];
+    const int tl = plen_slot(s);
+    uint8_t bad = 0;
+    // udpPacketsCanCoalesce (gro.go:519-544)
+    if (S.ipattr[bi] == S.ipattr[tgt] && (tl - (S.iph[bi] + 8)) % (int)S.it_gso[it] == 0 && S.gso[bi] <= S.it_gso[it]) {
+      // coalesceUDPPackets (gro.go:745-783)
+      const int hdrs = (uint8_t)(S.it_iph[it] + 8);
+      const int pay = plen_slot(bi) - hdrs;
+      if ((int)S.bcap[S.sbuf[s]] - offset < tl + pay) {
+      } else if (S.it_nm[it] == 0 && (S.it_bad[it] || !S.valid[s])) {
+      } else if (!S.valid[bi]) {
+        bad = 1;
+      } else {
+        S.pstart[bi] = (uint16_t)hdrs;
+        S.plen[bi] = (uint16_t)pay;
+        S.pnext[bi] = kNone;
+        S.pnext[S.stail[s]] = (int16_t)bi;
+        S.stail[s] = (int16_t)bi;
+        S.scount[s]++;
+        S.slen[s] += (uint32_t)pay;
+        S.it_nm[it]++;
+        return R_COALESCED;
+      }
+    }
+    insert(bi, f, bad);
+    return R_INSERT;
+  }
+
+  __device__ void run(bool raw) {
+    int nw = 0;
+    for (int i = 0; i < S.n_eff; ++i) {  // gro.go:1334-1363
+      int res = R_NOOP;
+      const int c = S.cand[i];
+      if (c != C_NOT && !S.noop[i]) res = c <= C_TCP6 ? tcp_gro(i) : udp_gro(i);
+      if (res == R_NOOP) S.szero[i] = 1;  // empty virtioNetHdr encoded into bufs[i] (:1350-1358)
+      if (res != R_COALESCED) S.to_write[nw++] = (int16_t)i;
+    }
+    S.n_write = raw ? 0 : nw;
+    // apply{TCP,UDP}Coalesce (gro.go:1364-1366), or -- after "invalid offset"
+    // -- nothing: the buffers keep what the coalescing wrote (appends, PSH)
+    for (int it = 0; it < S.n_items; ++it) {
+      if (!S.it_alive[it]) continue;
+      const int s = S.it_slot[it];
+      const int h = S.shead[s];
+      const bool changed = S.scount[s] > 1 || S.spsh[s];
+      if (raw ? !changed : S.it_nm[it] == 0) {
+        if (!raw) S.szero[s] = 1;  // numMerged == 0: empty virtioNetHdr (:1168-1174, :1250-1256)
+        continue;
+      }
+      materialize(S.sbuf[s], S.pnext[h], S.scount[s] - 1, S.plen[h], S.spsh[s], raw ? kNone : it);
+    }
+  }
+};
+
+// checksumValid (gro.go:554-612) of packet p on one 16-lane row (lane r):
+// pkt[iphLen:] summed in aligned 16-byte chunks, plus the pseudo header.
+__device__ bool row_checksum_valid(const uint8_t* pk, int pl, int iphl, bool v6, uint32_t proto, int r) {
+  const uint8_t* lo = pk + iphl;
+  const uint8_t* hi = pk + pl;
+  const uint8_t* a0 = reinterpret_cast<const uint8_t*>((uintptr_t)lo & ~(uintptr_t)15);
+  const int nch = (int)((hi - a0 + 15) >> 4);
+  uint64_t acc = 0;
+  for (int c = r; c < nch; c += 16) {
+    const uint4 v = ld16(a0 + 16 * c);
+    const int x0 = (int)(a0 - lo) + 16 * c;  // chunk position relative to the L4 start
+    acc += chunk_sum(v, x0, 0, pl - iphl);
+  }
+  uint32_t s = fold32_16(row16_sum_u32(fold64_16(acc)));
+  if (((uintptr_t)lo & 1u) == 0) s = bswap16(s);  // LE pairs at even addresses -> BE words from lo
+  // pseudo header: addresses (BE words), protocol, L4 length (gro.go:561-571)
+  const int a_lo = v6 ? 8 : 12, nw = v6 ? 16 : 4;
+  const uint32_t aw = r < nw ? be16g(pk + a_lo + 2 * r) : 0u;
+  const uint32_t ad = row16_sum_u32(aw);
+  const uint32_t t = fold32_16(s + fold32_16(ad) + proto + (uint32_t)((pl - iphl) & 0xFFFF));
+  return t == 0xFFFFu;
+}
+
+// Header byte x of an applied item before the two computed checksums
+// (applyTCPCoalesce / applyUDPCoalesce, gro.go:1099-1268).
+__device__ __forceinline__ uint32_t patched(uint32_t b, int x, int iphl, int csum_at, uint32_t pkt_len, bool v6,
+                                            bool udp, bool pshf) {
+  if (!v6) {
+    if (x == 2) b = pkt_len >> 8;  // total length (:1131 / :1214)
+    if (x == 3) b = pkt_len & 0xFF;
+    if (x == 10 || x == 11) b = 0;  // :1134 / :1217
+  } else {
+    const uint32_t pl = pkt_len - (uint32_t)iphl;  // payload length (:1124-1127 / :1207-1210)
+    if (x == 4) b = (pl >> 8) & 0xFF;
+    if (x == 5) b = pl & 0xFF;
+  }
+  if (udp) {
+    const uint32_t ul = pkt_len - (uint32_t)iphl;  // UDP length (:1229-1232)
+    if (x == iphl + 4) b = (ul >> 8) & 0xFF;
+    if (x == iphl + 5) b = ul & 0xFF;
+  } else if (pshf && x == iphl + 13) {
+    b |= 0x08;  // PSH of an appended packet (gro.go:724-729)
+  }
+  if (x == csum_at || x == csum_at + 1) b = 0;
+  return b;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ arena, wgcs_gro_buf* __restrict__ bufs,
+                                                        const wgcs_gro_call* __restrict__ calls,
+                                                        int32_t* __restrict__ status, int32_t* __restrict__ n_write,
+                                                        int32_t* __restrict__ to_write) {
+  __shared__ GroSmem S;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wv = t >> 6, r = lane & 15, row = t >> 4;
+  const wgcs_gro_call call = calls[blockIdx.x];
+  const int n = (int)call.n, offset = call.offset;
+  const bool can_udp = (call.flags & WGCS_GRO_CAN_UDP) != 0;
+  if (n > kMaxB || offset < 0) {  // block-uniform
+    if (t == 0) {
+      status[blockIdx.x] = WGCS_ERR_INVALID_ARG;
+      n_write[blockIdx.x] = 0;
+    }
+    return;
+  }
+  wgcs_gro_buf* cb = bufs + call.first;
+
+  // ---- 1. slice headers, handleGRO's offset check (gro.go:1335-1337)
+  if (t == 0) {
+    S.n_eff = n;
+    S.n_items = 0;
+    S.n_mat = 0;
+  }
+  __syncthreads();
+  if (t < n) {
+    const wgcs_gro_buf b = cb[t];
+    S.boff[t] = b.off;
+    S.blen[t] = b.len;
+    S.bcap[t] = b.cap;
+    if (offset < kVnet || (int64_t)offset > (int64_t)b.len - 1) atomicMin(&S.n_eff, t);
+  }
+  __syncthreads();
+  const int n_eff = S.n_eff;
+  if (t < n) {
+    S.sbuf[t] = (int16_t)t;
+    S.slen[t] = S.blen[t];
+    S.shead[t] = S.stail[t] = (int16_t)t;
+    S.scount[t] = 1;
+    S.pnext[t] = kNone;
+    S.pstart[t] = 0;
+    S.plen[t] = (uint16_t)(t < n_eff ? S.blen[t] - offset : 0);
+    S.spsh[t] = 0;
+    S.szero[t] = 0;
+    S.fl_head[t] = S.fl_tail[t] = kNone;
+    S.cand[t] = C_NOT;
+    S.noop[t] = 1;
+    S.valid[t] = 0;
+  }
+  // groCandidate + the tcpGRO / udpGRO checks that return groResultNoop
+  if (t < n_eff) {
+    const uint8_t* pk = arena + S.boff[t] + offset;
+    const uint32_t pl = S.blen[t] - (uint32_t)offset;
+    uint8_t c = C_NOT;
+    if (pl >= 28) {  // gro.go:1280-1317
+      const uint32_t v = pk[0] >> 4;
+      if (v == 4 && (pk[0] & 0x0F) == 5) {
+        if (pk[9] == 6 && pl >= 40) c = C_TCP4;
+        else if (pk[9] == 17 && can_udp) c = C_UDP4;
+      } else if (v == 6) {
+        if (pk[6] == 6 && pl >= 60) c = C_TCP6;
+        else if (pk[6] == 17 && pl >= 48 && can_udp) c = C_UDP6;
+      }
+    }
+    S.cand[t] = c;
+    if (c != C_NOT) {
+      const bool v6 = c == C_TCP6 || c == C_UDP6, tcp = c <= C_TCP6;
+      const int ih = v6 ? 40 : (pk[0] & 0x0F) * 4;
+      bool nop = pl > 65535;
+      if (v6) nop = nop || be16g(pk + 4) != pl - 40;
+      else nop = nop || be16g(pk + 2) != pl;
+      int thl = 8;
+      uint32_t fl = 0;
+      if (tcp) {
+        nop = nop || pl < (uint32_t)ih;
+        thl = (pk[ih + 12] >> 4) * 4;
+        nop = nop || thl < 20 || thl > 60 || pl < (uint32_t)(ih + thl);
+      } else {
+        nop = nop || pl < (uint32_t)(ih + 8);
+      }
+      if (!v6) nop = nop || (pk[6] & 0x20) || (uint8_t)(pk[6] << 3) || pk[7];  // fragments
+      if (!nop && tcp) {
+        fl = pk[ih + 13];
+        nop = fl != 0x10 && fl != 0x18;  // ACK, or ACK|PSH
+      }
+      const int g = nop ? 0 : (int)pl - ih - thl;
+      nop = nop || g < 1;
+      S.noop[t] = nop ? 1 : 0;
+      S.iph[t] = (uint8_t)ih;
+      S.th[t] = (uint8_t)thl;
+      S.psh[t] = (fl & 0x08) ? 1 : 0;
+      S.gso[t] = (uint16_t)g;
+      if (!nop) {
+        S.seq[t] = tcp ? be32g(pk + ih + 4) : 0u;
+        S.ipattr[t] = v6 ? (uint32_t)pk[0] | ((uint32_t)(pk[1] >> 4) << 8) | ((uint32_t)pk[7] << 16) | (6u << 24)
+                         : (uint32_t)pk[1] | ((uint32_t)(pk[6] >> 5) << 8) | ((uint32_t)pk[8] << 16) | (4u << 24);
+        // flow key hash: addresses, ports, ack (TCP), family and table
+        const int a_lo = v6 ? 8 : 12, al = v6 ? 16 : 4;
+        uint32_t h = 2166136261u;
+        for (int k = 0; k < 2 * al; ++k) h = fnv(h, pk[a_lo + k]);
+        for (int k = 0; k < 4; ++k) h = fnv(h, pk[ih + k]);
+        if (tcp)
+          for (int k = 8; k < 12; ++k) h = fnv(h, pk[ih + k]);
+        S.keyh[t] = fnv(h, c);
+        uint32_t oh = 2166136261u;
+        if (tcp)
+          for (int k = 20; k < thl; ++k) oh = fnv(oh, pk[ih + k]);
+        S.opth[t] = oh;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 2. flow ids (first earlier packet with the same key in the same table)
+  if (t < n_eff && S.cand[t] != C_NOT && !S.noop[t]) {
+    const uint8_t c = S.cand[t];
+    const bool v6 = c == C_TCP6 || c == C_UDP6, tcp = c <= C_TCP6;
+    const uint8_t* pk = arena + S.boff[t] + offset;
+    const int a_lo = v6 ? 8 : 12, al = v6 ? 16 : 4, ih = S.iph[t];
+    int f = t;
+    for (int q = 0; q < t; ++q) {
+      if (S.cand[q] != c || S.noop[q] || S.keyh[q] != S.keyh[t]) continue;
+      const uint8_t* pq = arena + S.boff[q] + offset;
+      const int iq = S.iph[q];
+      bool eq = true;
+      for (int k = 0; k < 2 * al && eq; ++k) eq = pk[a_lo + k] == pq[a_lo + k];
+      for (int k = 0; k < 4 && eq; ++k) eq = pk[ih + k] == pq[iq + k];
+      if (tcp)
+        for (int k = 8; k < 12 && eq; ++k) eq = pk[ih + k] == pq[iq + k];
+      if (eq) {
+        f = q;
+        break;
+      }
+    }
+    S.flow[t] = (uint16_t)f;
+  }
+  // checksumValid of every candidate: one 16-lane row per packet
+  for (int p = row; p < n_eff; p += 16) {  // row-uniform
+    if (S.cand[p] == C_NOT || S.noop[p]) continue;
+    const uint8_t c = S.cand[p];
+    const bool v6 = c == C_TCP6 || c == C_UDP6;
+    const bool ok = row_checksum_valid(arena + S.boff[p] + offset, (int)(S.blen[p] - offset), S.iph[p], v6,
+                                       c <= C_TCP6 ? 6u : 17u, r);
+    if (r == 0) S.valid[p] = ok ? 1 : 0;
+  }
+  __syncthreads();
+
+  // ---- 3. the handleGRO loop (thread 0)
+  const bool raw = n_eff < n;  // "invalid offset": coalescing happened, apply* did not
+  if (t == 0) {
+    Planner P{S, arena, offset};
+    P.run(raw);
+  }
+  __syncthreads();
+
+  // ---- 4. apply in place
+  // slice headers after the prepend swaps; toWrite; status
+  if (t < n) {
+    const int b = S.sbuf[t];
+    wgcs_gro_buf o;
+    o.off = S.boff[b];
+    o.len = S.slen[t];
+    o.cap = S.bcap[b];
+    cb[t] = o;
+  }
+  const int nw = S.n_write;
+  if (t < nw) to_write[call.first + t] = S.to_write[t];
+  if (t == 0) {
+    status[blockIdx.x] = raw ? WGCS_ERR_INVALID_OFFSET : 0;
+    n_write[blockIdx.x] = nw;
+  }
+  // empty virtio headers (NOOP buffers; unapplied items unless "invalid offset")
+  if (t < n && S.szero[t]) {
+    uint8_t* vh = arena + S.boff[S.sbuf[t]] + offset - kVnet;
+    for (int k = 0; k < kVnet; ++k) vh[k] = 0;
+  }
+  // materializations: one wave each -- the pieces appended behind the
+  // buffer's own packet (coalesce*Packets' appends, from the original packet
+  // bytes), then the item's apply* header rewrite + virtio header, or just the
+  // PSH the appends set
+  const int nm = S.n_mat;
+  for (int k = wv; k < nm; k += 4) {  // wave-uniform
+    const int buf = S.m_buf[k];
+    uint8_t* head = arena + S.boff[buf] + offset;
+    uint32_t pos = S.m_pos[k];
+    int p = S.m_first[k];
+    for (int q = 0; q < S.m_count[k]; ++q) {
+      copy_range(arena + S.boff[p] + offset + S.pstart[p], (int)S.plen[p], head + pos, lane);
+      pos += S.plen[p];
+      p = S.pnext[p];
+    }
+    const int it = S.m_item[k];
+    if (it < 0) {  // never applied: only the PSH that appends OR'ed in (gro.go:724-729)
+      if (lane == 0 && S.m_psh[k] && S.cand[buf] <= C_TCP6) head[S.iph[buf] + 13] |= 0x08;
+      continue;
+    }
+    const int s = S.it_slot[it];
+    const int ih = S.it_iph[it], hl = ih + S.it_l4h[it];
+    const uint8_t c = S.it_cand[it];
+    const bool v6 = c == C_TCP6 || c == C_UDP6, udp = c >= C_UDP4;
+    const bool pshf = S.m_psh[k] != 0;
+    const uint32_t pkt_len = S.slen[s] - (uint32_t)offset;
+    const int csum_at = ih + (udp ? 6 : 16);
+    const int x0 = 2 * lane;  // BE word x0 of the header, read before any write
+    uint32_t b0 = 0, b1 = 0;
+    if (x0 < hl) b0 = patched(head[x0], x0, ih, csum_at, pkt_len, v6, udp, pshf);
+    if (x0 + 1 < hl) b1 = patched(head[x0 + 1], x0 + 1, ih, csum_at, pkt_len, v6, udp, pshf);
+    const uint32_t w = (b0 << 8) | b1;
+    const int a_lo = v6 ? 8 : 12, a_hi = v6 ? 40 : 20;
+    const uint32_t ipc = (~fold32_16(wave_sum_u32(!v6 && x0 < ih ? w : 0u))) & 0xFFFFu;
+    // checksum([]byte{}, pseudoHeaderChecksumNoFold(src, dst, proto, len-iph)), not complemented
+    const uint32_t pcs = fold32_16(fold32_16(wave_sum_u32(x0 >= a_lo && x0 < a_hi ? w : 0u)) + (udp ? 17u : 6u) +
+                                   ((pkt_len - (uint32_t)ih) & 0xFFFFu));
+    if (!v6 && x0 == 10) {
+      b0 = ipc >> 8;
+      b1 = ipc & 0xFF;
+    }
+    if (x0 == csum_at) {
+      b0 = pcs >> 8;
+      b1 = pcs & 0xFF;
+    }
+    if (x0 < hl) head[x0] = (uint8_t)b0;
+    if (x0 + 1 < hl) head[x0 + 1] = (uint8_t)b1;
+    // virtio_net_hdr (gro.go:1107-1117 / :1191-1201), native byte order
+    if (lane < kVnet) {
+      const uint32_t gso_type = udp ? 5u : (v6 ? 4u : 1u);
+      const uint32_t f[5] = {(uint32_t)hl, S.it_gso[it], (uint32_t)ih, udp ? 6u : 16u, 0u};
+      uint32_t vb;
+      if (lane == 0) vb = 1;  // VIRTIO_NET_HDR_F_NEEDS_CSUM
+      else if (lane == 1) vb = gso_type;
+      else vb = (f[(lane - 2) >> 1] >> (8 * (lane & 1))) & 0xFF;
+      head[lane - kVnet] = (uint8_t)vb;
+    }
+  }
+}
+
+hipError_t launch_gro_batch(uint8_t* arena, wgcs_gro_buf* bufs, const wgcs_gro_call* calls, uint32_t n_calls,
+                            int32_t* status, int32_t* n_write, int32_t* to_write, hipStream_t s) {
+  if (n_calls == 0) return hipSuccess;
+  hipLaunchKernelGGL(gro_batch_kernel, dim3(n_calls), dim3(256), 0, s, arena, bufs, calls, status, n_write, to_write);
+  return hipGetLastError();
+}
+
+}  // namespace wgcs

@@ -169,3 +169,19 @@ extern "C" int wgcs_handle_gro(wgcs_ctx* ctx, uint8_t** bufs, size_t* lens, size
   for (int i : pl.to_write) to_write[(*n_to_write)++] = i;
   return bad_offset ? set_err(ctx, WGCS_ERR_INVALID_OFFSET, "invalid offset (packet %d)", n_eff) : WGCS_OK;
 }
+
+// Device-resident batch of Tun.Write calls: handleGRO per call, one workgroup
+// per call, everything in HBM (gro_batch_kernels.hip).
+extern "C" int wgcs_handle_gro_batch(wgcs_ctx* ctx, uint8_t* d_arena, wgcs_gro_buf* d_bufs,
+                                     const wgcs_gro_call* d_calls, uint32_t n_calls, int32_t* d_status,
+                                     int32_t* d_n_write, int32_t* d_to_write, void* stream) {
+  if (!ctx) return WGCS_ERR_INVALID_ARG;
+  if (n_calls == 0) return WGCS_OK;
+  if (!d_arena || !d_bufs || !d_calls || !d_status || !d_n_write || !d_to_write)
+    return set_err(ctx, WGCS_ERR_INVALID_ARG, "NULL pointer");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  const hipError_t e = launch_gro_batch(d_arena, d_bufs, d_calls, n_calls, d_status, d_n_write, d_to_write, s);
+  return e == hipSuccess ? WGCS_OK : hip_fail(ctx, e, "handle_gro_batch launch");
+}

@@ -105,6 +105,10 @@ struct GroSeg {
 // header) -- handleGRO stopped at an invalid offset before applyTCPCoalesce.
 enum : uint8_t { GRO_KIND_V6 = 1, GRO_KIND_UDP = 2, GRO_KIND_PSH = 4, GRO_KIND_RAW = 8 };
 
+// Device-resident batch of handleGRO calls (gro_batch_kernels.hip).
+hipError_t launch_gro_batch(uint8_t* arena, wgcs_gro_buf* bufs, const wgcs_gro_call* calls, uint32_t n_calls,
+                            int32_t* status, int32_t* n_write, int32_t* to_write, hipStream_t s);
+
 hipError_t launch_gro_coalesce(const uint8_t* stage, const GroItem* items, uint32_t n_items, const GroSeg* segs,
                                uint32_t n_segs, uint8_t* out, hipStream_t s);
 

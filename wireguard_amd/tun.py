@@ -44,6 +44,11 @@ def pkt_off(pkts: np.ndarray) -> np.ndarray:
     """Arena offsets of a PKT_DTYPE array (uint64)."""
     return pkts["off_lo"].astype(np.uint64) | (pkts["off_hi"].astype(np.uint64) << np.uint64(32))
 GSO_JOB_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("pad", "<u4")])
+# wgcs_gro_buf / wgcs_gro_call (include/wgcsum.h): a device-resident Tun.Write batch
+GRO_BUF_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("cap", "<u4")])
+GRO_CALL_DTYPE = np.dtype([("first", "<u4"), ("n", "<u4"), ("offset", "<i4"), ("flags", "<u4")])
+GRO_CAN_UDP = 0x1
+GRO_MAX_CALL = 256
 
 VIRTIO_NET_HDR_LEN = 10
 VIRTIO_NET_HDR_F_NEEDS_CSUM = 1
@@ -53,7 +58,8 @@ VIRTIO_NET_HDR_GSO_TCPV6 = 4
 VIRTIO_NET_HDR_GSO_UDP_L4 = 5
 
 __all__ = [
-    "Device", "Stager", "WriteStager", "PKT_DTYPE", "GSO_JOB_DTYPE", "MODE_FOLD", "MODE_L4_FILL", "MODE_VALIDATE", "MODE_PARTIAL",
+    "Device", "Stager", "WriteStager", "PKT_DTYPE", "GSO_JOB_DTYPE", "GRO_BUF_DTYPE", "GRO_CALL_DTYPE",
+    "GRO_CAN_UDP", "GRO_MAX_CALL", "MODE_FOLD", "MODE_L4_FILL", "MODE_VALIDATE", "MODE_PARTIAL",
     "MODE_IP4HDR", "F_INPLACE", "PKT_V6", "IPPROTO_TCP", "IPPROTO_UDP", "VirtioHdr", "WgcsError", "set_pkt_off",
     "pkt_off",
 ]
@@ -134,6 +140,14 @@ class Device:
         s = getattr(stream, "cuda_stream", stream)
         self._check(self.lib.wgcs_gso_split_batch(self.h, _ptr(arena), _ptr(jobs), n_jobs, _ptr(out), out_stride,
                                                   offset, max_segs, _ptr(sizes), _ptr(count), _ptr(status), s))
+
+    def handle_gro_batch(self, arena, bufs, calls, n_calls: int, status, n_write, to_write, stream=None) -> None:
+        """Device-resident batch of Tun.Write calls (wgcs_handle_gro_batch):
+        handleGRO per call, in place on `arena` and the GRO_BUF_DTYPE slice
+        headers `bufs`; per call status / n_write, toWrite in `to_write`."""
+        s = getattr(stream, "cuda_stream", stream)
+        self._check(self.lib.wgcs_handle_gro_batch(self.h, _ptr(arena), _ptr(bufs), _ptr(calls), n_calls, _ptr(status),
+                                                   _ptr(n_write), _ptr(to_write), s))
 
     # ------------------------------------------------------------ host batch
     def checksum_batch_host(self, mode: int, arena: np.ndarray, pkts: np.ndarray, initial=None,
