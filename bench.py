@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="cfg2",
-                    choices=sorted(CONFIGS) + ["cfg4", "gro", "gro_staged", "udp_split", "udp_coalesce"])
+                    choices=sorted(CONFIGS) + ["cfg4", "gro", "gro_staged", "gro_device", "udp_split", "udp_coalesce"])
     ap.add_argument("--mode", default="validate", choices=["validate", "fill"])
     ap.add_argument("--rotate", type=int, default=4, help="distinct batch copies (defeat the 256 MiB MALL)")
     ap.add_argument("--streams", type=int, default=0,
@@ -114,6 +114,10 @@ def main():
         from wireguard_amd import gro_bench
 
         return gro_bench.run_staged(args, torch, dev, dist, rank, world, local, barrier)
+    if args.config == "gro_device":
+        from wireguard_amd import gro_bench
+
+        return gro_bench.run_device(args, torch, dev, dist, rank, world, local, barrier)
     if args.config in ("udp_split", "udp_coalesce"):
         from wireguard_amd import udp_bench
 

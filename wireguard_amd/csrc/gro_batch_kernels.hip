@@ -14,10 +14,11 @@
 //      checksumValid (gro.go:554-612) of every candidate, one 16-lane DPP row
 //      per packet -- exact up front because the reference validates before it
 //      mutates (gro.go:665-681, :709-723, :767-775);
-//   3. thread 0 replays the loop of handleGRO over those precomputed fields:
-//      tcpGRO / udpGRO with the flow table as per-flow linked lists of items
-//      in LDS, coalesceTCPPackets / coalesceUDPPackets as piece lists (no byte
-//      moves yet), the prepend swaps of bufs, toWrite;
+//   3. the loop of handleGRO over those precomputed fields, one thread per
+//      flow (flows never interact): tcpGRO / udpGRO with the flow's items as a
+//      linked list in LDS, coalesceTCPPackets / coalesceUDPPackets as piece
+//      lists (no byte moves yet), the prepend swaps of bufs; toWrite in
+//      packet order by a wave ballot;
 //   4. every wave applies it in place, one buffer each: the pieces the
 //      reference appended behind the buffer's own packet (copied from the
 //      original packet bytes), then applyTCPCoalesce / applyUDPCoalesce's
@@ -61,7 +62,8 @@ struct GroSmem {
   uint8_t m_psh[2 * kMaxB];
   uint8_t cand[kMaxB], noop[kMaxB], iph[kMaxB], th[kMaxB], psh[kMaxB], valid[kMaxB], spsh[kMaxB], szero[kMaxB];
   uint8_t it_iph[kMaxB], it_l4h[kMaxB], it_psh[kMaxB], it_bad[kMaxB], it_alive[kMaxB], it_cand[kMaxB];
-  int n_eff, n_items, n_write, n_mat;
+  uint8_t res[kMaxB];                   // groResult of each packet (R_*)
+  int n_eff, n_write, n_mat;
 };
 
 __device__ __forceinline__ uint32_t be16g(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
@@ -69,7 +71,7 @@ __device__ __forceinline__ uint32_t be32g(const uint8_t* p) { return (be16g(p) <
 
 __device__ __forceinline__ uint32_t fnv(uint32_t h, uint32_t b) { return (h ^ b) * 16777619u; }
 
-// ---- thread 0: the handleGRO loop over the precomputed fields --------------
+// ---- the handleGRO loop over the precomputed fields (one thread per flow) ---
 
 struct Planner {
   GroSmem& S;
@@ -80,7 +82,7 @@ struct Planner {
   __device__ int plen_slot(int s) const { return (int)S.slen[s] - offset; }
 
   __device__ void insert(int bi, int f, uint8_t bad) {  // tcpGROTable.insert / udpGROTable.insert
-    const int it = S.n_items++;
+    const int it = bi;  // an item is named after the packet that inserted it
     S.it_slot[it] = (int16_t)bi;
     S.it_seq[it] = S.seq[bi];
     S.it_nm[it] = 0;
@@ -102,7 +104,7 @@ struct Planner {
   // followed by `count` pieces starting at node `first`; item >= 0: also the
   // apply* header rewrite and virtio header of that item.
   __device__ void materialize(int buf, int first, int count, uint32_t pos, uint8_t pshf, int item) {
-    const int k = S.n_mat++;
+    const int k = atomicAdd(&S.n_mat, 1);
     S.m_buf[k] = (int16_t)buf;
     S.m_first[k] = (int16_t)first;
     S.m_count[k] = (int16_t)count;
@@ -266,29 +268,29 @@ struct Planner {
     return R_INSERT;
   }
 
-  __device__ void run(bool raw) {
-    int nw = 0;
-    for (int i = 0; i < S.n_eff; ++i) {  // gro.go:1334-1363
-      int res = R_NOOP;
-      const int c = S.cand[i];
-      if (c != C_NOT && !S.noop[i]) res = c <= C_TCP6 ? tcp_gro(i) : udp_gro(i);
-      if (res == R_NOOP) S.szero[i] = 1;  // empty virtioNetHdr encoded into bufs[i] (:1350-1358)
-      if (res != R_COALESCED) S.to_write[nw++] = (int16_t)i;
+  // The loop of handleGRO (gro.go:1334-1363) restricted to the packets of
+  // one flow (first packet f).  Flows never interact: a packet only meets the
+  // items of its own flow key, and the buffers it swaps or appends into are
+  // its own flow's, so every flow of a call runs on its own thread.
+  __device__ void run_flow(int f) {
+    const bool tcp = S.cand[f] <= C_TCP6;
+    for (int i = f; i < S.n_eff; ++i) {
+      if (S.flow[i] != f || S.cand[i] == C_NOT || S.noop[i]) continue;
+      S.res[i] = (uint8_t)(tcp ? tcp_gro(i) : udp_gro(i));
     }
-    S.n_write = raw ? 0 : nw;
-    // apply{TCP,UDP}Coalesce (gro.go:1364-1366), or -- after "invalid offset"
-    // -- nothing: the buffers keep what the coalescing wrote (appends, PSH)
-    for (int it = 0; it < S.n_items; ++it) {
-      if (!S.it_alive[it]) continue;
-      const int s = S.it_slot[it];
-      const int h = S.shead[s];
-      const bool changed = S.scount[s] > 1 || S.spsh[s];
-      if (raw ? !changed : S.it_nm[it] == 0) {
-        if (!raw) S.szero[s] = 1;  // numMerged == 0: empty virtioNetHdr (:1168-1174, :1250-1256)
-        continue;
-      }
-      materialize(S.sbuf[s], S.pnext[h], S.scount[s] - 1, S.plen[h], S.spsh[s], raw ? kNone : it);
+  }
+
+  // apply{TCP,UDP}Coalesce (gro.go:1364-1366) for item `it`, or -- after
+  // "invalid offset" -- nothing: its buffer keeps what the coalescing wrote
+  __device__ void finish_item(int it, bool raw) {
+    const int s = S.it_slot[it];
+    const int h = S.shead[s];
+    const bool changed = S.scount[s] > 1 || S.spsh[s];
+    if (raw ? !changed : S.it_nm[it] == 0) {
+      if (!raw) S.szero[s] = 1;  // numMerged == 0: empty virtioNetHdr (:1168-1174, :1250-1256)
+      return;
     }
+    materialize(S.sbuf[s], S.pnext[h], S.scount[s] - 1, S.plen[h], S.spsh[s], raw ? kNone : it);
   }
 };
 
@@ -363,7 +365,6 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
   // ---- 1. slice headers, handleGRO's offset check (gro.go:1335-1337)
   if (t == 0) {
     S.n_eff = n;
-    S.n_items = 0;
     S.n_mat = 0;
   }
   __syncthreads();
@@ -390,6 +391,8 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
     S.cand[t] = C_NOT;
     S.noop[t] = 1;
     S.valid[t] = 0;
+    S.res[t] = R_NOOP;
+    S.it_alive[t] = 0;
   }
   // groCandidate + the tcpGRO / udpGRO checks that return groResultNoop
   if (t < n_eff) {
@@ -489,12 +492,26 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
   }
   __syncthreads();
 
-  // ---- 3. the handleGRO loop (thread 0)
+  // ---- 3. the handleGRO loop: one thread per flow
   const bool raw = n_eff < n;  // "invalid offset": coalescing happened, apply* did not
-  if (t == 0) {
-    Planner P{S, arena, offset};
-    P.run(raw);
+  Planner P{S, arena, offset};
+  if (t < n_eff && S.cand[t] != C_NOT && !S.noop[t] && S.flow[t] == t) P.run_flow(t);
+  __syncthreads();
+  // toWrite in packet order (groResultNoop and groResultTableInsert,
+  // gro.go:1349-1362); NOOP buffers get an empty virtioNetHdr (:1350-1358)
+  if (wv == 0) {
+    int base = 0;
+    for (int c0 = 0; c0 < n_eff; c0 += 64) {  // wave-uniform
+      const int p = c0 + lane;
+      const bool w = p < n_eff && S.res[p] != R_COALESCED;
+      const uint64_t m = __ballot(w);
+      if (w) S.to_write[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = (int16_t)p;
+      base += __popcll(m);
+    }
+    if (lane == 0) S.n_write = raw ? 0 : base;
   }
+  if (t < n_eff && S.res[t] == R_NOOP) S.szero[t] = 1;
+  if (t < n_eff && S.it_alive[t]) P.finish_item(t, raw);
   __syncthreads();
 
   // ---- 4. apply in place
