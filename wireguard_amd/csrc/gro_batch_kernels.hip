@@ -34,6 +34,7 @@
 #include "wgcs_common.h"
 #include "wgcs_copy.h"
 #include "wgcs_kernels.h"
+#include "wgcs_rows.h"
 
 namespace wgcs {
 
@@ -63,6 +64,8 @@ struct GroSmem {
   uint8_t cand[kMaxB], noop[kMaxB], iph[kMaxB], th[kMaxB], psh[kMaxB], valid[kMaxB], spsh[kMaxB], szero[kMaxB];
   uint8_t it_iph[kMaxB], it_l4h[kMaxB], it_psh[kMaxB], it_bad[kMaxB], it_alive[kMaxB], it_cand[kMaxB];
   uint8_t res[kMaxB];                   // groResult of each packet (R_*)
+  int16_t ndst[kMaxB];                  // piece p's destination buffer in its final item (-1: none)
+  uint32_t npos[kMaxB];                 // ... and its first byte there
   int n_eff, n_write, n_mat;
 };
 
@@ -290,22 +293,36 @@ struct Planner {
       if (!raw) S.szero[s] = 1;  // numMerged == 0: empty virtioNetHdr (:1168-1174, :1250-1256)
       return;
     }
-    materialize(S.sbuf[s], S.pnext[h], S.scount[s] - 1, S.plen[h], S.spsh[s], raw ? kNone : it);
+    // the item's pieces go behind its head packet: one row each (step 4)
+    uint32_t pos = S.plen[h];
+    for (int p = S.pnext[h]; p != kNone; p = S.pnext[p]) {
+      S.ndst[p] = S.sbuf[s];
+      S.npos[p] = pos;
+      pos += S.plen[p];
+    }
+    materialize(S.sbuf[s], kNone, 0, 0, S.spsh[s], raw ? kNone : it);
   }
 };
 
 // checksumValid (gro.go:554-612) of packet p on one 16-lane row (lane r):
 // pkt[iphLen:] summed in aligned 16-byte chunks, plus the pseudo header.
 __device__ bool row_checksum_valid(const uint8_t* pk, int pl, int iphl, bool v6, uint32_t proto, int r) {
+  constexpr int U = 6;  // 16-byte chunks per lane in flight: a 1536-byte packet in one batch
   const uint8_t* lo = pk + iphl;
   const uint8_t* hi = pk + pl;
   const uint8_t* a0 = reinterpret_cast<const uint8_t*>((uintptr_t)lo & ~(uintptr_t)15);
   const int nch = (int)((hi - a0 + 15) >> 4);
+  const int x00 = (int)(a0 - lo);  // position of chunk 0 relative to the L4 start
   uint64_t acc = 0;
-  for (int c = r; c < nch; c += 16) {
-    const uint4 v = ld16(a0 + 16 * c);
-    const int x0 = (int)(a0 - lo) + 16 * c;  // chunk position relative to the L4 start
-    acc += chunk_sum(v, x0, 0, pl - iphl);
+  for (int c0 = 0; c0 < nch; c0 += 16 * U) {  // row-uniform
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + r + 16 * u;
+      v[u] = c < nch ? ld16(a0 + 16 * c) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += chunk_sum(v[u], x00 + 16 * (c0 + r + 16 * u), 0, pl - iphl);
   }
   uint32_t s = fold32_16(row16_sum_u32(fold64_16(acc)));
   if (((uintptr_t)lo & 1u) == 0) s = bswap16(s);  // LE pairs at even addresses -> BE words from lo
@@ -315,6 +332,50 @@ __device__ bool row_checksum_valid(const uint8_t* pk, int pl, int iphl, bool v6,
   const uint32_t ad = row16_sum_u32(aw);
   const uint32_t t = fold32_16(s + fold32_16(ad) + proto + (uint32_t)((pl - iphl) & 0xFFFF));
   return t == 0xFFFFu;
+}
+
+// n bytes src -> dst on one 16-lane row (lane r), any alignments: destination
+// chunk k (16-byte aligned) = bytes [sb, sb + 16) of the dword-aligned source
+// window k and the first dword of window k + 1 (the next lane's, DPP row_ror);
+// all windows of a 1536-byte piece in flight at once.
+__device__ void row_copy(const uint8_t* src, int n, uint8_t* dst, int r) {
+  constexpr int U = 6;
+  const int dalign = (int)((uintptr_t)dst & 15u);
+  uint8_t* dbase = dst - dalign;
+  const int nk = (n + dalign + 15) >> 4;
+  const uint8_t* w0 = src - dalign;  // source of destination chunk 0's first byte
+  const int sb = (int)((uintptr_t)w0 & 3u);
+  const uint8_t* abase = w0 - sb;
+  const uint8_t* src_hi = src + n;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  for (int k0 = 0; k0 < nk; k0 += 16 * U) {  // row-uniform
+    uint4 A[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint8_t* ca = abase + 16 * (k0 + r + 16 * u);
+      A[u] = (ca < src_hi && ca + 16 > src) ? ld_window<false>(ca, src_hi) : z;
+    }
+    uint32_t E = 0;
+    if (r == 15) {
+      const uint8_t* ce = abase + 16 * (k0 + 16 * U);
+      if (ce < src_hi) E = *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(ce, 4));
+    }
+    uint32_t Rc = row_next(A[0].x);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + r + 16 * u;
+      const uint32_t Rx = u + 1 < U ? row_next(A[u + 1 < U ? u + 1 : u].x) : E;
+      const uint32_t nx = r == 15 ? Rx : Rc;
+      Rc = Rx;
+      if (k < nk) {
+        const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(A[u].y, A[u].x, sb),
+                                   __builtin_amdgcn_alignbyte(A[u].z, A[u].y, sb),
+                                   __builtin_amdgcn_alignbyte(A[u].w, A[u].z, sb),
+                                   __builtin_amdgcn_alignbyte(nx, A[u].w, sb));
+        store_chunk(dbase + 16 * k, v, 16 * k - dalign, n);
+      }
+    }
+  }
 }
 
 // Header byte x of an applied item before the two computed checksums
@@ -393,6 +454,7 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
     S.valid[t] = 0;
     S.res[t] = R_NOOP;
     S.it_alive[t] = 0;
+    S.ndst[t] = kNone;
   }
   // groCandidate + the tcpGRO / udpGRO checks that return groResultNoop
   if (t < n_eff) {
@@ -539,13 +601,19 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
   // buffer's own packet (coalesce*Packets' appends, from the original packet
   // bytes), then the item's apply* header rewrite + virtio header, or just the
   // PSH the appends set
+  // final items' pieces: one 16-lane row per piece
+  for (int p = row; p < n_eff; p += 16) {  // row-uniform
+    const int d = S.ndst[p];
+    if (d == kNone) continue;
+    row_copy(arena + S.boff[p] + offset + S.pstart[p], (int)S.plen[p], arena + S.boff[d] + offset + S.npos[p], r);
+  }
   const int nm = S.n_mat;
   for (int k = wv; k < nm; k += 4) {  // wave-uniform
     const int buf = S.m_buf[k];
     uint8_t* head = arena + S.boff[buf] + offset;
     uint32_t pos = S.m_pos[k];
     int p = S.m_first[k];
-    for (int q = 0; q < S.m_count[k]; ++q) {
+    for (int q = 0; q < S.m_count[k]; ++q) {  // a buffer a prepend moved out: its appends, in order
       copy_range(arena + S.boff[p] + offset + S.pstart[p], (int)S.plen[p], head + pos, lane);
       pos += S.plen[p];
       p = S.pnext[p];
