@@ -213,7 +213,7 @@ typedef struct wgcs_gro_call {
   uint32_t flags; /* WGCS_GRO_CAN_UDP */
 } wgcs_gro_call;
 #define WGCS_GRO_CAN_UDP 0x1u
-#define WGCS_GRO_MAX_CALL 256
+#define WGCS_GRO_MAX_CALL 128 /* conn.BatchSize (conn/conn.go:14): the largest Write batch */
 int wgcs_handle_gro_batch(wgcs_ctx *ctx, uint8_t *d_arena, wgcs_gro_buf *d_bufs, const wgcs_gro_call *d_calls,
                           uint32_t n_calls, int32_t *d_status, int32_t *d_n_write, int32_t *d_to_write,
                           void *stream);

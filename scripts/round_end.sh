@@ -45,6 +45,7 @@ if want lines; then
   line cfg1 300 --config cfg1 --steps 200 --warmup 20 --cpu-seconds 4
   line gro 300 --config gro --steps 200 --warmup 20 --cpu-seconds 3
   line gro_staged 300 --config gro_staged --steps 30 --warmup 5 --cpu-seconds 3
+  line gro_device 300 --config gro_device --steps 40 --warmup 4 --cpu-seconds 3
   line udp_split 300 --config udp_split --steps 50 --warmup 5 --cpu-seconds 3
   line udp_coalesce 300 --config udp_coalesce --steps 50 --warmup 5 --cpu-seconds 3
 fi

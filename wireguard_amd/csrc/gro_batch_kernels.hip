@@ -52,15 +52,18 @@ struct GroSmem {
   uint64_t boff[kMaxB];                 // arena offset of each original buffer
   uint32_t blen[kMaxB], bcap[kMaxB];    // its slice length / capacity
   uint32_t seq[kMaxB], ipattr[kMaxB], keyh[kMaxB], opth[kMaxB];
+  uint32_t kw[kMaxB][10];               // flow key words: addresses, ports, ack (TCP)
   uint32_t slen[kMaxB];                 // len(bufs[s]) of the slice now at position s
   uint32_t it_seq[kMaxB];
-  uint32_t m_pos[2 * kMaxB];            // materializations: first byte of the pieces in the buffer
+  uint32_t m_pos[kMaxB];            // materializations: first byte of the pieces in the buffer
   uint16_t gso[kMaxB], flow[kMaxB], pstart[kMaxB], plen[kMaxB], it_nm[kMaxB], it_gso[kMaxB];
   int16_t pnext[kMaxB], sbuf[kMaxB], shead[kMaxB], stail[kMaxB];
   int16_t it_slot[kMaxB], it_prev[kMaxB], it_next[kMaxB], fl_head[kMaxB], fl_tail[kMaxB];
   int16_t to_write[kMaxB], scount[kMaxB];
-  int16_t m_buf[2 * kMaxB], m_first[2 * kMaxB], m_count[2 * kMaxB], m_item[2 * kMaxB];  // m_item: -1 = plain
-  uint8_t m_psh[2 * kMaxB];
+  // materializations (<= n: one per final item or per prepend, each the
+  // work of a distinct packet); m_item: -1 = plain
+  int16_t m_buf[kMaxB], m_first[kMaxB], m_count[kMaxB], m_item[kMaxB];
+  uint8_t m_psh[kMaxB];
   uint8_t cand[kMaxB], noop[kMaxB], iph[kMaxB], th[kMaxB], psh[kMaxB], valid[kMaxB], spsh[kMaxB], szero[kMaxB];
   uint8_t it_iph[kMaxB], it_l4h[kMaxB], it_psh[kMaxB], it_bad[kMaxB], it_alive[kMaxB], it_cand[kMaxB];
   uint8_t res[kMaxB];                   // groResult of each packet (R_*)
@@ -503,14 +506,25 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
         S.seq[t] = tcp ? be32g(pk + ih + 4) : 0u;
         S.ipattr[t] = v6 ? (uint32_t)pk[0] | ((uint32_t)(pk[1] >> 4) << 8) | ((uint32_t)pk[7] << 16) | (6u << 24)
                          : (uint32_t)pk[1] | ((uint32_t)(pk[6] >> 5) << 8) | ((uint32_t)pk[8] << 16) | (4u << 24);
-        // flow key hash: addresses, ports, ack (TCP), family and table
-        const int a_lo = v6 ? 8 : 12, al = v6 ? 16 : 4;
+        // flow key words (addresses, ports, ack for TCP) into LDS + their hash;
+        // the byte loads are independent (fixed trip counts)
+        const int a_lo = v6 ? 8 : 12, nab = v6 ? 32 : 8;
         uint32_t h = 2166136261u;
-        for (int k = 0; k < 2 * al; ++k) h = fnv(h, pk[a_lo + k]);
-        for (int k = 0; k < 4; ++k) h = fnv(h, pk[ih + k]);
-        if (tcp)
-          for (int k = 8; k < 12; ++k) h = fnv(h, pk[ih + k]);
-        S.keyh[t] = fnv(h, c);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+          uint32_t x = 0;
+          if (4 * w < nab)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x = (x << 8) | pk[a_lo + 4 * w + k];
+          if (4 * w < nab) {
+            S.kw[t][w] = x;
+            h = fnv(h, x);
+          }
+        }
+        const uint32_t ports = be32g(pk + ih), ack = tcp ? be32g(pk + ih + 8) : 0u;
+        S.kw[t][nab / 4] = ports;
+        S.kw[t][nab / 4 + 1] = ack;
+        S.keyh[t] = fnv(fnv(fnv(h, ports), ack), c);
         uint32_t oh = 2166136261u;
         if (tcp)
           for (int k = 20; k < thl; ++k) oh = fnv(oh, pk[ih + k]);
@@ -524,18 +538,14 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
   if (t < n_eff && S.cand[t] != C_NOT && !S.noop[t]) {
     const uint8_t c = S.cand[t];
     const bool v6 = c == C_TCP6 || c == C_UDP6, tcp = c <= C_TCP6;
-    const uint8_t* pk = arena + S.boff[t] + offset;
-    const int a_lo = v6 ? 8 : 12, al = v6 ? 16 : 4, ih = S.iph[t];
+    const int nkw = v6 ? 10 : 4;  // key words: the class fixes the layout (ack is 0 for UDP)
+    (void)tcp;
+    const uint32_t kh = S.keyh[t];
     int f = t;
     for (int q = 0; q < t; ++q) {
-      if (S.cand[q] != c || S.noop[q] || S.keyh[q] != S.keyh[t]) continue;
-      const uint8_t* pq = arena + S.boff[q] + offset;
-      const int iq = S.iph[q];
+      if (S.keyh[q] != kh || S.cand[q] != c || S.noop[q]) continue;
       bool eq = true;
-      for (int k = 0; k < 2 * al && eq; ++k) eq = pk[a_lo + k] == pq[a_lo + k];
-      for (int k = 0; k < 4 && eq; ++k) eq = pk[ih + k] == pq[iq + k];
-      if (tcp)
-        for (int k = 8; k < 12 && eq; ++k) eq = pk[ih + k] == pq[iq + k];
+      for (int w = 0; w < nkw; ++w) eq = eq && S.kw[q][w] == S.kw[t][w];
       if (eq) {
         f = q;
         break;

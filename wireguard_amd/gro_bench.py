@@ -230,7 +230,7 @@ def cpu_baseline(pkts, seconds):
                           "sample": f"{calls_mt} calls on {threads} pthreads, each on a private copy of the batch"}}
 
 
-def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int = 512, rotate: int = 4):
+def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int = 1280, rotate: int = 4):
     """bench.py --config gro_device: the device-resident batch of Tun.Write
     calls (wgcs_handle_gro_batch).  One step = one launch over `calls` calls
     of the 128-packet batch above, every buffer a Go-sized slice (cap 65,551 B)
@@ -238,8 +238,11 @@ def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int =
     (handleGRO rewrites headers), so the bench keeps `rotate` copies and
     restores them between bursts of `rotate` launches, outside the timed
     region; the timed region is the launches, bracketed by a device sync."""
+    import os
+
     from .tun import GRO_BUF_DTYPE, GRO_CALL_DTYPE, GRO_CAN_UDP
 
+    calls = int(os.environ.get("WGCS_GRO_CALLS", calls))
     pkts = make_batch(dev)
     n = len(pkts)
     N = calls * n

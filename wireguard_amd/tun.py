@@ -48,7 +48,7 @@ GSO_JOB_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("pad", "<u4")])
 GRO_BUF_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("cap", "<u4")])
 GRO_CALL_DTYPE = np.dtype([("first", "<u4"), ("n", "<u4"), ("offset", "<i4"), ("flags", "<u4")])
 GRO_CAN_UDP = 0x1
-GRO_MAX_CALL = 256
+GRO_MAX_CALL = 128
 
 VIRTIO_NET_HDR_LEN = 10
 VIRTIO_NET_HDR_F_NEEDS_CSUM = 1
