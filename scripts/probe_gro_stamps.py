@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Phase timeline of gro_batch_kernel (timing-only build with -DWGCS_P_STAMPS:
-thread 0 writes s_memtime at each phase boundary into to_write[first+100+k],
-which the cfg's 128-packet calls never use).  Prints, over all calls of one
+"""Phase timeline of gro_batch_kernel (timing-only build with -DWGCS_P_STAMPS,
+a switch that existed only in the experimental revision this was run against:
+thread 0 wrote s_memtime at each phase boundary into to_write[first+100+k],
+which the cfg's 128-packet calls never use; output in
+profiles/r2_probe_gro_stamps.jsonl).  Prints, over all calls of one
 launch, the median cycles per phase.  Build: python scripts/probe_gro_stamps.py build"""
 import json
 import os
