@@ -5,6 +5,7 @@ Each variant is the library built with timing-only -D switches that existed
 only in the experimental revisions of gso_kernels.hip this script was run
 against (wrong output by design, except `base`; the switches were removed
 with the experiment, the outputs are kept in profiles/r2_probe_gso_*.jsonl):
+  WGCS_P_NT=false    regular (temporal) payload loads instead of non-temporal
   WGCS_P_NTST        non-temporal payload stores
   WGCS_P_U=n         n payload windows per lane in flight (default 6)
   WGCS_P_NODEC       the decoder wave publishes the rows' own geometry instead
@@ -30,10 +31,7 @@ sys.path.insert(0, ROOT)
 OUTDIR = os.path.join(ROOT, "scripts", "probe_so")
 VARIANTS = {
     "base": [],
-    "ntst": ["WGCS_P_NTST"],
-    "u4": ["WGCS_P_U=4"],
-    "u8": ["WGCS_P_U=8"],
-    "u3": ["WGCS_P_U=3"],
+    "rt_loads": ["WGCS_P_NT=false"],
 }
 
 
