@@ -6,6 +6,10 @@ only in the experimental revisions of gso_kernels.hip this script was run
 against (wrong output by design, except `base`; the switches were removed
 with the experiment, the outputs are kept in profiles/r2_probe_gso_*.jsonl):
   WGCS_P_NT=false    regular (temporal) payload loads instead of non-temporal
+  WGCS_P_PLAINLD     first payload batch without ld_window's page-crossing test
+  WGCS_P_PLAINST     full 16-byte stores for every payload chunk (no partial-chunk pieces)
+  WGCS_P_OLDTAIL     the segment's last partial chunk as byte/short/dword pieces instead of one
+                     full store merged with the slot's bytes read ahead
   WGCS_P_NTST        non-temporal payload stores
   WGCS_P_U=n         n payload windows per lane in flight (default 6)
   WGCS_P_NODEC       the decoder wave publishes the rows' own geometry instead
@@ -30,8 +34,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUTDIR = os.path.join(ROOT, "scripts", "probe_so")
 VARIANTS = {
-    "base": [],
-    "rt_loads": ["WGCS_P_NT=false"],
+    "tail_merge": [],
+    "tail_pieces": ["WGCS_P_OLDTAIL"],
 }
 
 
