@@ -132,3 +132,52 @@ def test_gro_batch_rejects_oversized_call(dev):
     meta, offs, host_bufs, lens_all, arena0, arena, gb, st, nw, tw = _run(dev, calls)
     assert st[0] == -1 and nw[0] == 0  # WGCS_ERR_INVALID_ARG, nothing touched
     assert np.array_equal(arena, arena0)
+
+
+def test_gro_batch_host_test_scenarios(dev):
+    """Every scenario of tests/test_gpu_gro.py (the host-path GRO tests) as
+    one call each, all in one launch."""
+    rng = np.random.default_rng(11)
+    s_pre = flow(6, seed=3)
+    s_bad = flow(8, seed=5)
+    for k in (0, 3, 7):
+        b = bytearray(s_bad[k]); b[-1] ^= 0x5A; s_bad[k] = bytes(b)
+    u_bad = flow(6, udp=True, seed=6)
+    b = bytearray(u_bad[2]); b[-2] ^= 1; u_bad[2] = bytes(b)
+    flows = [flow(int(rng.integers(1, 10)), seg=int(rng.choice([536, 1000, 1448])), v6=bool(k % 2),
+                  udp=bool(k % 3 == 0), seed=100 + k, last_flags=int(rng.choice([0x10, 0x18]))) for k in range(10)]
+    icmp = bytearray(flows[0][0]); icmp[9] = 1
+    opts = bytearray(flows[1][0] if not flows[1][0][0] >> 4 == 6 else flows[0][0]); opts[0] = 0x46
+    frag = bytearray(flows[0][0]); frag[6] = 0x20
+    batch = [p for f in flows for p in f] + [bytes(icmp), bytes(opts), bytes(frag)]
+    order = np.argsort(rng.random(len(batch)) + np.arange(len(batch)) * 0.05)
+    mixed = [batch[i] for i in order]
+    for _ in range(5):
+        k = int(rng.integers(0, len(mixed)))
+        b = bytearray(mixed[k]); b[-1] ^= 0x11; mixed[k] = bytes(b)
+    a, u, o = flow(6, seed=21, last_flags=0x18), flow(4, udp=True, seed=22), flow(4, seed=23)
+    inv = [a[0], a[1], u[0], o[1], o[0], a[2], u[1], a[3], o[2], a[4], u[2], a[5], o[3], u[3]]
+    ic2 = bytearray(a[0]); ic2[9] = 1
+    inv.insert(3, bytes(ic2))
+    big = []
+    for k in range(16):
+        big += flow(8, seg=1400, v6=bool(k % 2), udp=bool(k % 4 == 3), seed=200 + k)
+    perm = np.random.default_rng(12).permutation(len(big))
+    calls = [
+        (flow(8), 65535, True, None),
+        (flow(12, seg=1200, seed=7), 65535, True, None),
+        (flow(12, seg=1200, v6=True, seed=7), 65535, True, None),
+        (flow(12, seg=1200, udp=True, seed=7), 65535, True, None),
+        (flow(12, seg=1200, v6=True, udp=True, seed=7), 65535, True, None),
+        ([s_pre[2], s_pre[1], s_pre[0], s_pre[3], s_pre[5], s_pre[4]], 65535, True, None),
+        (flow(5, seg=1000, seed=4, last_flags=0x18), 65535, True, None),
+        (flow(3, seg=700, seed=4) + flow(3, seg=1000, seed=4), 65535, True, None),
+        (s_bad, 65535, True, None),
+        (u_bad, 65535, True, None),
+        (flow(6, seg=1000, seed=8), lambda n: OFFSET + n + 1500, True, None),
+        (flow(4, udp=True, seed=9), 65535, False, None),
+        (mixed, 65535, True, None),
+        ([big[i] for i in perm], 65535, True, None),
+        (big, 65535, True, None),
+    ] + [(inv, 65535, True, {bad_at: OFFSET}) for bad_at in (1, 5, 9, 13)]
+    assert _check(dev, calls) == len(calls)
