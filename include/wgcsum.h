@@ -4,7 +4,8 @@
  *
  * Plain C types only (pointers and sizes); no torch, no HIP types in the
  * signatures (streams are passed as `void*` = hipStream_t, NULL = the
- * context's own stream).  Every entry point is thread-safe: calls on one
+ * context's own stream, a blocking stream: ordered both ways with work on the
+ * HIP null stream, e.g. torch's default stream).  Every entry point is thread-safe: calls on one
  * context are serialized by a context mutex (the reference serializes Read
  * with Tun.readMu and Write with Tun.writeMu, tun/tun.go:101,:105).
  *

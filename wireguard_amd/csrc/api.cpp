@@ -87,7 +87,10 @@ int wgcs_init(int device, wgcs_ctx** out) {
   if (!ctx) return WGCS_ERR_NOMEM;
   ctx->device = device;
   hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  // A blocking stream: work a caller queued on the HIP null stream (torch's
+  // default stream) before a NULL-stream call is ordered before it, and after
+  // it is ordered after it.
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault);
   hipDeviceProp_t prop;
   if (e == hipSuccess) e = hipGetDeviceProperties(&prop, device);
   if (e != hipSuccess) {
