@@ -17,6 +17,8 @@ with the experiment, the outputs are kept in profiles/r2_probe_gso_*.jsonl):
   WGCS_P_CONSTJOB    the rows take cfg4's job descriptor and virtio header as
                      constants (no dependent loads before the payload loads)
   WGCS_P_NOBAR       no decoder, no LDS barrier: the rows use their own geometry
+  WGCS_P_A16=0/1     payload windows dword-aligned (alignbyte + 1 DPP dword) or
+                     16-byte aligned (funnel + 4 DPP dwords)
 (An earlier run of this script timed a two-kernel design -- plan kernel +
 segment kernel -- with switches that no longer exist; its output is
 profiles/r2_probe_gso_plan_kernel.jsonl.)
@@ -34,8 +36,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUTDIR = os.path.join(ROOT, "scripts", "probe_so")
 VARIANTS = {
-    "tail_merge": [],
-    "tail_pieces": ["WGCS_P_OLDTAIL"],
+    "a4_windows": ["WGCS_P_A16=0"],
+    "a16_windows": ["WGCS_P_A16=1"],
 }
 
 
