@@ -11,12 +11,19 @@ with the experiment, the outputs are kept in profiles/r2_probe_gso_*.jsonl):
   WGCS_P_OLDTAIL     the segment's last partial chunk as byte/short/dword pieces instead of one
                      full store merged with the slot's bytes read ahead
   WGCS_P_NTST        non-temporal payload stores
-  WGCS_P_U=n         n payload windows per lane in flight (default 6)
+  WGCS_P_U=n         n payload windows per lane in flight (default 6; now the
+                     product tunable WGCS_GSO_U)
   WGCS_P_NODEC       the decoder wave publishes the rows' own geometry instead
                      of decoding (no validation, zero header constants)
   WGCS_P_CONSTJOB    the rows take cfg4's job descriptor and virtio header as
                      constants (no dependent loads before the payload loads)
   WGCS_P_NOBAR       no decoder, no LDS barrier: the rows use their own geometry
+  WGCS_P_WPE=n       amdgpu_waves_per_eu(n): VGPR budget for n waves per SIMD
+                     (now the product tunable WGCS_GSO_WAVES, default 5)
+  WGCS_P_BUF=0/1     payload windows through flat global loads (page test per
+                     window) or raw buffer loads over the job's bytes (range check)
+  WGCS_P_EARLY=0/1   first payload batch issued before (1) or after (0) the
+                     data-offset check (the decoded path is an out-of-line call)
   WGCS_P_A16=0/1     payload windows dword-aligned (alignbyte + 1 DPP dword) or
                      16-byte aligned (funnel + 4 DPP dwords)
 (An earlier run of this script timed a two-kernel design -- plan kernel +
@@ -36,8 +43,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUTDIR = os.path.join(ROOT, "scripts", "probe_so")
 VARIANTS = {
-    "a4_windows": ["WGCS_P_A16=0"],
-    "a16_windows": ["WGCS_P_A16=1"],
+    "head": None,  # the committed kernel, built from `git archive HEAD` (see build())
+    "w5": ["WGCS_GSO_WAVES=5"],
+    "w5_u8": ["WGCS_GSO_WAVES=5", "WGCS_GSO_U=8"],
+    "w5_u4": ["WGCS_GSO_WAVES=5", "WGCS_GSO_U=4"],
+    "w4": ["WGCS_GSO_WAVES=4"],
 }
 
 
@@ -47,7 +57,15 @@ def build():
     os.makedirs(OUTDIR, exist_ok=True)
     for k, defs in VARIANTS.items():
         out = os.path.join(OUTDIR, f"libwgcsum_{k}.so")
-        B.build(out=out, extra=[f"-D{d}" for d in defs])
+        if defs is None:  # HEAD's sources, unpacked by the caller into /tmp/headtree
+            csrc = B.CSRC
+            B.CSRC = "/tmp/headtree/wireguard_amd/csrc"
+            try:
+                B.build(out=out)
+            finally:
+                B.CSRC = csrc
+        else:
+            B.build(out=out, extra=[f"-D{d}" for d in defs])
         print("built", out, flush=True)
 
 

@@ -360,17 +360,16 @@ __device__ void none_segment(const uint8_t* rb, const Job& j, uint8_t* dst, int 
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// Row-per-segment split: one 16-lane DPP row per OUTPUT segment, 64 rows per
-// 1024-thread block (wave 0 decodes the job once, LDS broadcast); grid =
-// (job, group of 64 segments).  Per row:
-//   * the first U payload windows are loaded speculatively (gsoSize only)
-//     before the decode finishes; further batches follow the decoded bounds;
-//   * the header source chunks are fetched after the barrier (L2 hits);
-//   * destination chunk k = r + 16u is assembled from the dword-aligned source
-//     window k and the next lane's first dword (DPP row_ror:15) with a per-row
-//     byte shift, summed (v_dot2) and stored as one dwordx4;
+// Row-per-segment split: one 16-lane DPP row per OUTPUT segment, 16 rows per
+// 256-thread block; grid = (job, group of 16 segments).  Per row:
+//   * payload windows are dword-aligned 16-byte raw buffer loads over the
+//     job's bytes (range-checked: nothing past the job is touched, no page
+//     test), U per lane in flight;
+//   * destination chunk k = r + 16u is assembled from window k and the next
+//     lane's first dword (DPP row_ror:15) with a per-row byte shift, summed
+//     (v_dot2) and stored as one dwordx4 (byte-exact pieces at the edges);
 //   * the checksums come from the row sum plus job constants plus the
-//     rewritten field values (gro.go:1419-1465), and the header chunks are
+//     rewritten field values (gro.go:1419-1465), and the header bytes are
 //     stored last with both checksums filled in.
 // Each output byte is written exactly once, each input byte read once.
 
@@ -495,42 +494,57 @@ struct JobInfo {
 
 __device__ __forceinline__ int ufl(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
+// Buffer resource over one job's bytes [vb, vb + jlen): every dword holding a
+// job byte passes the range check (num_records jlen + 3), loads past it
+// return zeros instead of touching memory past the arena.  Built from
+// wave-uniform values only (one descriptor per wave, no waterfall).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t job_rsrc(const uint8_t* vb, uint32_t jlen) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vb), (short)0, (int)(jlen + 3u), 0x00020000);
+}
+template <bool NT>
+__device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t rs, int off) {
+  const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, NT ? 2 : 0);
+  return make_uint4(t[0], t[1], t[2], t[3]);
+}
+// One batch of dword-aligned windows: lane r loads windows k0 + r + 16u at job
+// offset aoff + 16 * window (lane 15 also the first dword of the window after
+// the batch, E), each only when it overlaps the job bytes [lo, hi).
+template <int U, bool NT>
+__device__ __forceinline__ void load_windows(__amdgpu_buffer_rsrc_t rs, int aoff, int k0, int r, int lo, int hi,
+                                             uint4 (&A)[U], uint32_t& E) {
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  const int o0 = aoff + 16 * (k0 + r);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int o = o0 + 256 * u;
+    A[u] = (o < hi && o + 16 > lo) ? bld16<NT>(rs, o) : z;
+  }
+  E = 0;
+  const int oe = aoff + 16 * (k0 + 16 * U);
+  if (r == 15 && oe < hi && oe + 4 > lo) E = __builtin_amdgcn_raw_buffer_load_b32(rs, oe, 0, NT ? 2 : 0);
+}
+
 // One row's payload stream: destination chunk k = bytes [sb, sb + 16) of the
 // dword-aligned source window k and the first dword of window k + 1 (next
 // lane, DPP row_ror).  Sums the L4 bytes [hdrLen, pktLen) from the same
-// registers (v_dot2), stores every chunk past the header chunks (k >= hk) and
-// keeps the payload part of header chunk r in `keep`.  The first batch of
-// windows may already be in A/E (loaded == true).
+// registers (v_dot2) and stores the payload bytes of every chunk (those of a
+// chunk shared with the header as byte-exact pieces; the header phase stores
+// the chunk's header bytes).
 template <int U, bool NT>
 __device__ __forceinline__ void stream_row(const uint8_t* rb, int i, int gso, int hdr_len, int plen, int dalign,
-                                           uint8_t* dbase, int r, uint4 (&A)[U], uint32_t& E, bool loaded,
-                                           uint32_t& acc, uint4& keep) {
+                                           uint8_t* dbase, int r, uint32_t& acc, __amdgpu_buffer_rsrc_t rs) {
   const int seg_start = hdr_len + i * gso;
   const int seg_end = min(plen, seg_start + gso);
   const int pkt_len = hdr_len + (seg_end - seg_start);
   const int nk = (pkt_len + dalign + 15) >> 4;
-  const int hk = min((hdr_len + dalign + 15) >> 4, nk);
-  const uint8_t* src_lo = rb + seg_start;
-  const uint8_t* src_hi = rb + seg_end;
   const uint8_t* w0 = rb + (int64_t)i * gso - dalign;  // source of destination chunk 0 (payload positions)
   const int sb = (int)((uintptr_t)w0 & 3u);
-  const uint8_t* abase = w0 - sb;
-  const uint4 z = make_uint4(0, 0, 0, 0);
+  const int aoff = (int)(w0 - sb - (rb - 10));         // its dword-aligned window, job-relative
   acc = 0;
-  keep = z;
   for (int k0 = 0; k0 < nk; k0 += 16 * U) {
-    if (k0 > 0 || !loaded) {  // wave-uniform
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint8_t* ca = abase + 16 * (k0 + r + 16 * u);
-        A[u] = (ca < src_hi && ca + 16 > src_lo) ? ld_window<NT>(ca, src_hi) : z;
-      }
-      E = 0;
-      if (r == 15) {
-        const uint8_t* ce = abase + 16 * (k0 + 16 * U);
-        if (ce < src_hi && ce + 4 > src_lo) E = *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(ce, 4));
-      }
-    }
+    uint4 A[U];
+    uint32_t E;
+    load_windows<U, NT>(rs, aoff, k0, r, 10 + seg_start, 10 + seg_end, A, E);
     uint32_t Rc = row_next(A[0].x);  // lane 15: lane 0's next-u dword
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -546,8 +560,11 @@ __device__ __forceinline__ void stream_row(const uint8_t* rb, int i, int gso, in
         const int x0 = 16 * k - dalign;
         if (x0 >= hdr_len && x0 + 16 <= pkt_len) acc = add4(acc, v);
         else acc = add4_masked(acc, v, byte_bits16(hdr_len - x0, pkt_len - x0), false);
-        if (k < hk) keep = v;
-        else store_chunk(dbase + 16 * k, v, x0, pkt_len);
+        // the chunk's address formed here, not hoisted for all U chunks up front
+        // (six 64-bit addresses held across the stream cost an occupancy step)
+        int ko = 16 * k;
+        asm volatile("" : "+v"(ko));
+        store_chunk(dbase + ko, v, x0 - hdr_len, pkt_len - hdr_len);  // bytes [hdrLen, pktLen)
       }
     }
   }
@@ -636,15 +653,200 @@ __device__ __noinline__ void decode_publish(const uint8_t* vb, uint32_t jlen, ui
 // through LDS; after the barrier each row follows that verdict (nothing on an
 // error, the byte-granular general path, or the stream with the decoded
 // geometry and the general header path).
+// The segment's header chunk and checksums, given the row's payload sum
+// `acc` and the job-constant header values: on the fast layout the header
+// chunk in packet coordinates (Q) rewritten field by field and shifted to the
+// destination phase; otherwise a byte-exact replay of the reference's write
+// order on the chunk in destination coordinates.  Stores the header bytes
+// [0, hdrLen) of the segment (the stream stored the rest) and its size.
+__device__ __forceinline__ void finish_row(bool fast, const uint4 Q, int type, int ipv, int hdr_len, int gso, int cs,
+                                           int co, int plen, int i, int r, int dalign, const uint8_t* dst,
+                                           uint8_t* dbase, uint32_t acc, uint32_t ip_base, uint32_t l4_base,
+                                           uint32_t tflags, uint32_t id0, uint32_t seq0, int32_t* size_out) {
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  // ---- segment geometry (row-uniform)
+  const bool v4 = ipv == 4, tcp = type != GSO_UDP_L4;
+  const int csum_at = (cs + co) & 0xFFFF;
+  const int seg_start = hdr_len + i * gso;
+  const int seg_end = min(plen, seg_start + gso);
+  const int seg_len = seg_end - seg_start;
+  const int pkt_len = hdr_len + seg_len;
+  const bool last = seg_end == plen;
+  const int nk = (pkt_len + dalign + 15) >> 4;
+  const int hk = min((hdr_len + dalign + 15) >> 4, nk);
+  const uint32_t id = i > 0 ? ((id0 + 1) & 0xFFFFu) : id0;  // quirk: id0 + 1 for every i >= 1 (:1426-1431)
+  const uint32_t seq = seq0 + (uint32_t)(uint16_t)((uint16_t)gso * (uint16_t)i);  // uint16 product (:1445)
+  const uint32_t ulen = (uint32_t)(uint16_t)(seg_len + (hdr_len - cs));           // UDP length (:1462-1465)
+  const uint32_t tlen = (uint32_t)(uint16_t)(hdr_len - cs + seg_len);             // transportLen (:1469-1471)
+  const uint32_t proto = tcp ? 6u : 17u;
+  const int x0h = 16 * r - dalign;
+
+  if (fast) {
+    // ---- sums: payload (row reduction) + job constants + rewritten fields
+    uint32_t t_pay = fold32_16(row16_sum_u32(acc));
+    if ((((uintptr_t)dst + (uintptr_t)cs) & 1u) == 0) t_pay = bswap16(t_pay);  // pairing from csumStart
+    const uint32_t var = tcp ? (seq >> 16) + (seq & 0xFFFFu) + (last ? (tflags & 0x09u) : 0u) : ulen;
+    const uint32_t l4c = (~fold32_16(t_pay + l4_base + var + proto + tlen)) & 0xFFFFu;
+    // ---- header chunk in packet coordinates, rewritten (gro.go:1418-1465, :1486-1490)
+    uint4 P = Q;
+    if (v4) {
+      const uint32_t ipc = (~fold32_16(ip_base + (uint32_t)pkt_len + id)) & 0xFFFFu;
+      put_be16_u(P, r, 2, (uint32_t)pkt_len);  // total length (:1433)
+      put_be16_u(P, r, 4, id);                 // identification (:1426-1431)
+      put_be16_u(P, r, 10, ipc);               // header checksum (:1434-1436)
+    } else {
+      put_be16_u(P, r, 4, (uint32_t)(pkt_len - cs));  // payload length (:1439)
+    }
+    if (tcp) {
+      put_be16_u(P, r, cs + 4, seq >> 16);  // sequence number (:1445-1446)
+      put_be16_u(P, r, cs + 6, seq);
+      put_u(P, r, cs + 13, last ? tflags : (tflags & ~0x09u), 0xFFu);  // FIN|PSH on the last only (:1447-1459)
+    } else {
+      put_be16_u(P, r, cs + 4, ulen);
+    }
+    put_be16_u(P, r, csum_at, l4c);  // L4 checksum (:1486-1490)
+    // ---- to the destination phase (previous chunk of the row: DPP row_shr:1),
+    // merged with the payload bytes, stored
+    const uint4 Pp = row_prev4(P);
+    const uint4 D = dalign ? funnel_v(Pp, P, 16 - dalign) : P;
+    if (r < hk) store_chunk(dbase + 16 * r, D, x0h, hdr_len);  // header bytes [0, hdrLen)
+  } else {
+    // ---- general header path (unusual csum offsets): byte-exact replay of
+    // the reference's write order on the chunk (destination coordinates)
+    const int a_lo = v4 ? 12 : 8, a_hi = v4 ? 20 : 40;
+    uint32_t acc_ip = 0;
+    uint4 hv = z;
+    if (r < hk) {
+      hv = Q;
+      // readBuf's zeroed fields (gro.go:1388,:1393), then the per-segment header writes in order
+      if (v4) put_be16(hv, x0h, 10, 0, hdr_len);
+      put_be16(hv, x0h, csum_at, 0, hdr_len);
+      if (v4) {
+        put_be16(hv, x0h, 4, id, hdr_len);
+        put_be16(hv, x0h, 2, pkt_len, hdr_len);
+      } else {
+        put_be16(hv, x0h, 4, pkt_len - cs, hdr_len);
+      }
+      if (tcp) {
+        put_be16(hv, x0h, cs + 4, seq >> 16, hdr_len);
+        put_be16(hv, x0h, cs + 6, seq, hdr_len);
+        const int fl = cs + 13 - x0h;
+        if (!last && cs + 13 < hdr_len && fl >= 0 && fl < 16) hv = set_chunk_byte(hv, fl, chunk_byte(hv, fl) & ~0x09u);
+      } else {
+        put_be16(hv, x0h, cs + 4, ulen, hdr_len);
+      }
+      if (v4) acc_ip = add4_masked(0u, hv, byte_bits16(-x0h, cs - x0h), false);
+      acc = add4_masked(acc, hv, byte_bits16(cs - x0h, hdr_len - x0h), false);
+      acc = add4_masked(acc, hv, byte_bits16(a_lo - x0h, a_hi - x0h), (cs & 1) != 0);  // pseudo-header addresses
+    }
+    uint32_t t_ip = fold32_16(row16_sum_u32(acc_ip));
+    if ((((uintptr_t)dst) & 1u) == 0) t_ip = bswap16(t_ip);
+    uint32_t t_l4 = fold32_16(row16_sum_u32(acc));
+    if ((((uintptr_t)dst + (uintptr_t)cs) & 1u) == 0) t_l4 = bswap16(t_l4);
+    const uint32_t l4c = (~fold32_16(t_l4 + proto + tlen)) & 0xFFFFu;
+    if (r < hk) {
+      if (v4) put_be16(hv, x0h, 10, (~t_ip) & 0xFFFFu, hdr_len);
+      put_be16(hv, x0h, csum_at, l4c, hdr_len);
+      store_chunk(dbase + 16 * r, hv, x0h, hdr_len);  // header bytes [0, hdrLen)
+    }
+  }
+  if (r == 0) *size_out = pkt_len;
+}
+
+// Every job that is not clean (GSO_NONE, errors, unusual geometry): wave 0
+// runs the full validation (decode_publish) and publishes its verdict through
+// LDS, the rows follow it.  Out of line, so that its registers do not count
+// against the clean path's occupancy (it spills, if at all, only here).
 template <int U, bool NT>
-__global__ __launch_bounds__(256) void gso_rows_kernel(const uint8_t* __restrict__ arena,
+__device__ __noinline__ void decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, uint32_t jflags_a, uint32_t room,
+                                          uint32_t max_segs, int i, bool first_block, int32_t* count_j,
+                                          int32_t* status_j, uint8_t* out0, uint8_t* dst, int32_t* sizes_j) {
+  __shared__ JobInfo ji;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15;
+  const int wv = threadIdx.x >> 6;
+  // the job's values are wave-uniform (arguments arrive in VGPRs)
+  const uint64_t vbu = ((uint64_t)(uint32_t)ufl((int)(uint32_t)(uintptr_t)vb_a)) |
+                       ((uint64_t)(uint32_t)ufl((int)(uint32_t)((uintptr_t)vb_a >> 32)) << 32);
+  const uint8_t* vb = reinterpret_cast<const uint8_t*>(vbu);
+  const uint32_t jlen = (uint32_t)ufl((int)jlen_a), jflags = (uint32_t)ufl((int)jflags_a);
+  const uint8_t* rb = vb + 10;
+  const int dalign = (int)((uintptr_t)dst & 15u);
+  uint8_t* dbase = dst - dalign;
+  const int hph = (int)((uintptr_t)rb & 15u);
+  const uint8_t* hab = rb - hph + 16 * r;
+  // ---- decoded path: wave 0 decodes, every wave follows its verdict
+  if (wv == 0) decode_publish(vb, jlen, jflags, room, max_segs, lane, &ji, first_block, count_j, status_j);
+  lds_barrier();  // the decoder's verdict
+  const int st = ufl(ji.status);
+  const int nseg = ufl(ji.nseg);
+  const uint32_t shape = (uint32_t)ufl((int)ji.shape);
+  const int type = (int)(shape & 0xFFu);
+  if ((st != 0 && st != WGCS_ERR_TOO_MANY_SEGMENTS) || nseg == 0) return;
+  const int plen = ufl(ji.plen);
+  if (type == GSO_NONE) {  // one packet into bufs[0], by wave 0 of the job's first block
+    if (first_block && wv == 0) {
+      Job jn = {};
+      jn.flags = ufl(ji.flags);
+      jn.cs = ufl(ji.cs);
+      jn.co = ufl(ji.co);
+      jn.plen = plen;
+      none_segment(rb, jn, out0, lane);
+      if (lane == 0) *sizes_j = plen;
+    }
+    return;
+  }
+  if (i >= nseg) return;  // whole rows retire; DPP below stays inside live rows
+  const int ipv = (int)((shape >> 8) & 0xFFu);
+  const bool fast = (shape >> 24) != 0;
+  const int hdr_len = ufl(ji.hdr_len);
+  const int gso = ufl(ji.gso);
+  const int cs = ufl(ji.cs);
+  const int co = ufl(ji.co);
+  if ((shape >> 16) & 0xFFu) {  // block-uniform
+    gso_general_row(rb, plen, type, ipv, hdr_len, gso, cs, co, i, dst, r, sizes_j + i);
+    return;
+  }
+  uint32_t acc = 0;
+  stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen));
+  // header chunks: packet coordinates on the fast layout, destination
+  // coordinates for the general header path
+  const uint8_t* hend = rb + hdr_len;
+  const int hphd = (int)((uintptr_t)(rb - dalign) & 15u);
+  const uint8_t* hb2 = fast ? hab : rb - dalign - hphd + 16 * r;
+  uint4 H0 = z, H1 = z;
+  if (hb2 < hend && hb2 + 16 > rb) H0 = ld16(hb2);
+  if (hb2 + 16 < hend && hb2 + 32 > rb) H1 = ld16(hb2 + 16);
+  const uint4 Q = fast ? funnel(H0, H1, hph) : funnel_v(H0, H1, hphd);
+  const uint32_t ip_base = (uint32_t)ufl((int)ji.ip_base);
+  const uint32_t l4_base = (uint32_t)ufl((int)ji.l4_base);
+  const uint32_t tflags = (uint32_t)ufl((int)ji.tflags);
+  const uint32_t id0 = (uint32_t)ufl((int)ji.id0);
+  const uint32_t seq0 = (uint32_t)ufl((int)ji.seq0);
+  finish_row(fast, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base, tflags,
+             id0, seq0, sizes_j + i);
+}
+
+// Build-time tunables (defaults measured on cfg4):
+// payload windows per lane in flight, and the occupancy the kernel is compiled
+// for.  The out-of-line decoded path would otherwise set the register count
+// (151 VGPRs, 3 waves per SIMD); at 5 waves (<= 96 VGPRs) the clean path runs
+// without spills and the decoded path spills only inside its own call.
+#ifndef WGCS_GSO_U
+#define WGCS_GSO_U 6
+#endif
+#ifndef WGCS_GSO_WAVES
+#define WGCS_GSO_WAVES 5
+#endif
+template <int U, bool NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WAVES, 8))) void gso_rows_kernel(const uint8_t* __restrict__ arena,
                                                        const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
                                                        uint8_t* __restrict__ out, uint32_t out_stride,
                                                        const GsoOutPos* __restrict__ outpos, uint32_t offset,
                                                        uint32_t room, int32_t* __restrict__ sizes,
                                                        int32_t* __restrict__ count, int32_t* __restrict__ status) {
   constexpr int ROWS = 16;
-  __shared__ JobInfo ji;
   const int lane = threadIdx.x & 63;
   const int r = lane & 15;
   const int wv = threadIdx.x >> 6;
@@ -717,25 +919,6 @@ __global__ __launch_bounds__(256) void gso_rows_kernel(const uint8_t* __restrict
   const int nseg_s = min(nfull_s, (int)max_segs);
   const bool live_s = clean_s && i < nseg_s;  // row-uniform
 
-  // ---- first payload batch (needs gsoSize only), then the header chunks in
-  // packet coordinates (L2 hits shared by the job's rows)
-  uint4 A[U];
-  uint32_t E = 0;
-  if (live_s) {
-    const uint8_t* w0 = rb + (int64_t)i * gso_s - dalign;
-    const uint8_t* abase = w0 - ((uintptr_t)w0 & 3u);
-    const uint8_t* src_lo = rb + hdr_s + i * gso_s;
-    const uint8_t* src_hi = rb + min(plen_s, hdr_s + (i + 1) * gso_s);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint8_t* ca = abase + 16 * (r + 16 * u);
-      A[u] = (ca < src_hi && ca + 16 > src_lo) ? ld_window<NT>(ca, src_hi) : z;
-    }
-    if (r == 15) {
-      const uint8_t* ce = abase + 16 * (16 * U);
-      if (ce < src_hi && ce + 4 > src_lo) E = *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(ce, 4));
-    }
-  }
   uint4 Q = funnel(H0, H1, hph);  // readBuf[16r, 16r + 16) (bytes below hdrLen)
   // the TCP data offset decides hdrLen (tun.go:601-614): block-uniform verdict
   bool clean = clean_s;
@@ -744,183 +927,55 @@ __global__ __launch_bounds__(256) void gso_rows_kernel(const uint8_t* __restrict
     clean = ((cs_s + th) & 0xFFFF) == hdr_s;
   }
 
-  uint32_t acc = 0;
-  uint4 keep = z;
-  int type = type_s, ipv = ipv_s, hdr_len = hdr_s, gso = gso_s, cs = cs_s, co = co_s, plen = plen_s;
-  bool fast = true;
-  uint32_t ip_base = 0, l4_base = 0, tflags = 0, id0 = 0, seq0 = 0;
-  if (clean) {
+  // The payload loads are issued only after this verdict: no payload window
+  // is live across the decoded path's call, so the clean path's registers
+  // stay its own (the verdict waits on the header chunks, which arrive with
+  // the virtio header).  readfirstlane makes the branch provably uniform.
+  if (ufl(clean ? 1 : 0)) {
     if (blockIdx.y == 0 && threadIdx.x == 0) {  // the checks can only end in the segment count here
       const bool many = nfull_s > (int)max_segs;
       count[jb] = many ? (int)max_segs - 1 : nfull_s;
       status[jb] = many ? WGCS_ERR_TOO_MANY_SEGMENTS : 0;
     }
-    if (!live_s) return;
-  } else {
-    // ---- decoded path: wave 0 decodes, every wave follows its verdict
-    if (wv == 0) decode_publish(vb, jlen, job.flags, room, max_segs, lane, &ji, blockIdx.y == 0, &count[jb], &status[jb]);
-    lds_barrier();  // the decoder's verdict
-    const int st = ufl(ji.status);
-    const int nseg = ufl(ji.nseg);
-    const uint32_t shape = (uint32_t)ufl((int)ji.shape);
-    type = (int)(shape & 0xFFu);
-    if ((st != 0 && st != WGCS_ERR_TOO_MANY_SEGMENTS) || nseg == 0) return;
-    plen = ufl(ji.plen);
-    if (type == GSO_NONE) {  // one packet into bufs[0], by wave 0 of the job's first block
-      if (blockIdx.y == 0 && wv == 0) {
-        Job jn = {};
-        jn.flags = ufl(ji.flags);
-        jn.cs = ufl(ji.cs);
-        jn.co = ufl(ji.co);
-        jn.plen = plen;
-        none_segment(rb, jn, out + obase + offset, lane);
-        if (lane == 0) sizes[slot0] = plen;
+    if (live_s) {
+      // ---- the payload stream
+      const int type = type_s, ipv = ipv_s, hdr_len = hdr_s, gso = gso_s, cs = cs_s, co = co_s, plen = plen_s;
+      uint32_t acc = 0;
+      stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen));
+      uint32_t ip_base = 0, l4_base = 0, tflags = 0, id0 = 0, seq0 = 0;
+      {
+      // job-constant header sums from this row's own header chunks (header_fast's
+      // values): IPv4 header without total length / id / checksum, the L4
+      // header from csumStart without checksum field, seq / UDP length and the
+      // flags byte, and the pseudo-header addresses, each as BE words
+      const int x0 = 16 * r;
+      const bool tcp_c = type != GSO_UDP_L4;
+      const int vlo = cs + 4, vhi = tcp_c ? cs + 8 : cs + 6;
+      const int ca = (cs + co) & 0xFFFF;
+      if (ipv == 4) {
+        const uint32_t m = byte_bits16(-x0, cs - x0) & ~byte_bits16(2 - x0, 6 - x0) & ~byte_bits16(10 - x0, 12 - x0);
+        ip_base = (uint32_t)ufl((int)bswap16(fold32_16(row16_sum_u32(add4_masked(0u, Q, m, false)))));
       }
-      return;
-    }
-    if (i >= nseg) return;  // whole rows retire; DPP below stays inside live rows
-    ipv = (int)((shape >> 8) & 0xFFu);
-    fast = (shape >> 24) != 0;
-    hdr_len = ufl(ji.hdr_len);
-    gso = ufl(ji.gso);
-    cs = ufl(ji.cs);
-    co = ufl(ji.co);
-    if ((shape >> 16) & 0xFFu) {  // block-uniform
-      gso_general_row(rb, plen, type, ipv, hdr_len, gso, cs, co, i, dst, r, &sizes[slot0 + (uint32_t)i]);
-      return;
-    }
-  }
-  // ---- the payload stream (the clean path's first batch is already in A / E)
-  stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, A, E, clean, acc, keep);
-  if (clean) {
-    // job-constant header sums from this row's own header chunks (header_fast's
-    // values): IPv4 header without total length / id / checksum, the L4
-    // header from csumStart without checksum field, seq / UDP length and the
-    // flags byte, and the pseudo-header addresses, each as BE words
-    const int x0 = 16 * r;
-    const bool tcp_c = type != GSO_UDP_L4;
-    const int vlo = cs + 4, vhi = tcp_c ? cs + 8 : cs + 6;
-    const int ca = (cs + co) & 0xFFFF;
-    if (ipv == 4) {
-      const uint32_t m = byte_bits16(-x0, cs - x0) & ~byte_bits16(2 - x0, 6 - x0) & ~byte_bits16(10 - x0, 12 - x0);
-      ip_base = (uint32_t)ufl((int)bswap16(fold32_16(row16_sum_u32(add4_masked(0u, Q, m, false)))));
-    }
-    uint32_t ml4 = byte_bits16(cs - x0, hdr_len - x0) & ~byte_bits16(ca - x0, ca + 2 - x0) &
-                   ~byte_bits16(vlo - x0, vhi - x0);
-    if (tcp_c) ml4 &= ~byte_bits16(cs + 13 - x0, cs + 14 - x0);
-    const int a_lo = ipv == 4 ? 12 : 8, a_hi = ipv == 4 ? 20 : 40;
-    uint32_t s4 = add4_masked(0u, Q, ml4, false);
-    s4 = add4_masked(s4, Q, byte_bits16(a_lo - x0, a_hi - x0), (cs & 1) != 0);
-    uint32_t t4 = fold32_16(row16_sum_u32(s4));
-    if ((cs & 1) == 0) t4 = bswap16(t4);  // pairing from csumStart (packet coordinates)
-    if (tcp_c) tflags = qbyte(Q, cs + 13);
-    l4_base = (uint32_t)ufl((int)t4) + (tflags & ~0x09u);
-    if (ipv == 4) id0 = (qbyte(Q, 4) << 8) | qbyte(Q, 5);
-    if (tcp_c) seq0 = (qbyte(Q, vlo) << 24) | (qbyte(Q, vlo + 1) << 16) | (qbyte(Q, vlo + 2) << 8) | qbyte(Q, vlo + 3);
-  } else {
-    const uint8_t* hend = rb + hdr_len;
-    const int hphd = (int)((uintptr_t)(rb - dalign) & 15u);
-    const uint8_t* hb2 = fast ? hab : rb - dalign - hphd + 16 * r;
-    H0 = z;
-    H1 = z;
-    if (hb2 < hend && hb2 + 16 > rb) H0 = ld16(hb2);
-    if (hb2 + 16 < hend && hb2 + 32 > rb) H1 = ld16(hb2 + 16);
-    Q = fast ? funnel(H0, H1, hph) : funnel_v(H0, H1, hphd);
-    ip_base = (uint32_t)ufl((int)ji.ip_base);
-    l4_base = (uint32_t)ufl((int)ji.l4_base);
-    tflags = (uint32_t)ufl((int)ji.tflags);
-    id0 = (uint32_t)ufl((int)ji.id0);
-    seq0 = (uint32_t)ufl((int)ji.seq0);
-  }
-
-  // ---- segment geometry (row-uniform)
-  const bool v4 = ipv == 4, tcp = type != GSO_UDP_L4;
-  const int csum_at = (cs + co) & 0xFFFF;
-  const int seg_start = hdr_len + i * gso;
-  const int seg_end = min(plen, seg_start + gso);
-  const int seg_len = seg_end - seg_start;
-  const int pkt_len = hdr_len + seg_len;
-  const bool last = seg_end == plen;
-  const int nk = (pkt_len + dalign + 15) >> 4;
-  const int hk = min((hdr_len + dalign + 15) >> 4, nk);
-  const uint32_t id = i > 0 ? ((id0 + 1) & 0xFFFFu) : id0;  // quirk: id0 + 1 for every i >= 1 (:1426-1431)
-  const uint32_t seq = seq0 + (uint32_t)(uint16_t)((uint16_t)gso * (uint16_t)i);  // uint16 product (:1445)
-  const uint32_t ulen = (uint32_t)(uint16_t)(seg_len + (hdr_len - cs));           // UDP length (:1462-1465)
-  const uint32_t tlen = (uint32_t)(uint16_t)(hdr_len - cs + seg_len);             // transportLen (:1469-1471)
-  const uint32_t proto = tcp ? 6u : 17u;
-  const int x0h = 16 * r - dalign;
-  const uint32_t hmask = byte_bits16(-x0h, hdr_len - x0h);  // header positions of destination chunk r
-
-  if (fast) {
-    // ---- sums: payload (row reduction) + job constants + rewritten fields
-    uint32_t t_pay = fold32_16(row16_sum_u32(acc));
-    if ((((uintptr_t)dst + (uintptr_t)cs) & 1u) == 0) t_pay = bswap16(t_pay);  // pairing from csumStart
-    const uint32_t var = tcp ? (seq >> 16) + (seq & 0xFFFFu) + (last ? (tflags & 0x09u) : 0u) : ulen;
-    const uint32_t l4c = (~fold32_16(t_pay + l4_base + var + proto + tlen)) & 0xFFFFu;
-    // ---- header chunk in packet coordinates, rewritten (gro.go:1418-1465, :1486-1490)
-    uint4 P = Q;
-    if (v4) {
-      const uint32_t ipc = (~fold32_16(ip_base + (uint32_t)pkt_len + id)) & 0xFFFFu;
-      put_be16_u(P, r, 2, (uint32_t)pkt_len);  // total length (:1433)
-      put_be16_u(P, r, 4, id);                 // identification (:1426-1431)
-      put_be16_u(P, r, 10, ipc);               // header checksum (:1434-1436)
-    } else {
-      put_be16_u(P, r, 4, (uint32_t)(pkt_len - cs));  // payload length (:1439)
-    }
-    if (tcp) {
-      put_be16_u(P, r, cs + 4, seq >> 16);  // sequence number (:1445-1446)
-      put_be16_u(P, r, cs + 6, seq);
-      put_u(P, r, cs + 13, last ? tflags : (tflags & ~0x09u), 0xFFu);  // FIN|PSH on the last only (:1447-1459)
-    } else {
-      put_be16_u(P, r, cs + 4, ulen);
-    }
-    put_be16_u(P, r, csum_at, l4c);  // L4 checksum (:1486-1490)
-    // ---- to the destination phase (previous chunk of the row: DPP row_shr:1),
-    // merged with the payload bytes, stored
-    const uint4 Pp = row_prev4(P);
-    const uint4 D = dalign ? funnel_v(Pp, P, 16 - dalign) : P;
-    if (r < hk) store_chunk(dbase + 16 * r, select_bytes(D, keep, hmask), x0h, pkt_len);
-  } else {
-    // ---- general header path (unusual csum offsets): byte-exact replay of
-    // the reference's write order on the chunk (destination coordinates)
-    const int a_lo = v4 ? 12 : 8, a_hi = v4 ? 20 : 40;
-    uint32_t acc_ip = 0;
-    uint4 hv = z;
-    if (r < hk) {
-      hv = select_bytes(Q, keep, hmask);
-      // readBuf's zeroed fields (gro.go:1388,:1393), then the per-segment header writes in order
-      if (v4) put_be16(hv, x0h, 10, 0, hdr_len);
-      put_be16(hv, x0h, csum_at, 0, hdr_len);
-      if (v4) {
-        put_be16(hv, x0h, 4, id, hdr_len);
-        put_be16(hv, x0h, 2, pkt_len, hdr_len);
-      } else {
-        put_be16(hv, x0h, 4, pkt_len - cs, hdr_len);
+      uint32_t ml4 = byte_bits16(cs - x0, hdr_len - x0) & ~byte_bits16(ca - x0, ca + 2 - x0) &
+                     ~byte_bits16(vlo - x0, vhi - x0);
+      if (tcp_c) ml4 &= ~byte_bits16(cs + 13 - x0, cs + 14 - x0);
+      const int a_lo = ipv == 4 ? 12 : 8, a_hi = ipv == 4 ? 20 : 40;
+      uint32_t s4 = add4_masked(0u, Q, ml4, false);
+      s4 = add4_masked(s4, Q, byte_bits16(a_lo - x0, a_hi - x0), (cs & 1) != 0);
+      uint32_t t4 = fold32_16(row16_sum_u32(s4));
+      if ((cs & 1) == 0) t4 = bswap16(t4);  // pairing from csumStart (packet coordinates)
+      if (tcp_c) tflags = qbyte(Q, cs + 13);
+      l4_base = (uint32_t)ufl((int)t4) + (tflags & ~0x09u);
+      if (ipv == 4) id0 = (qbyte(Q, 4) << 8) | qbyte(Q, 5);
+      if (tcp_c) seq0 = (qbyte(Q, vlo) << 24) | (qbyte(Q, vlo + 1) << 16) | (qbyte(Q, vlo + 2) << 8) | qbyte(Q, vlo + 3);
       }
-      if (tcp) {
-        put_be16(hv, x0h, cs + 4, seq >> 16, hdr_len);
-        put_be16(hv, x0h, cs + 6, seq, hdr_len);
-        const int fl = cs + 13 - x0h;
-        if (!last && cs + 13 < hdr_len && fl >= 0 && fl < 16) hv = set_chunk_byte(hv, fl, chunk_byte(hv, fl) & ~0x09u);
-      } else {
-        put_be16(hv, x0h, cs + 4, ulen, hdr_len);
-      }
-      if (v4) acc_ip = add4_masked(0u, hv, byte_bits16(-x0h, cs - x0h), false);
-      acc = add4_masked(acc, hv, byte_bits16(cs - x0h, hdr_len - x0h), false);
-      acc = add4_masked(acc, hv, byte_bits16(a_lo - x0h, a_hi - x0h), (cs & 1) != 0);  // pseudo-header addresses
+      finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base, tflags,
+                 id0, seq0, &sizes[slot0 + (uint32_t)i]);
     }
-    uint32_t t_ip = fold32_16(row16_sum_u32(acc_ip));
-    if ((((uintptr_t)dst) & 1u) == 0) t_ip = bswap16(t_ip);
-    uint32_t t_l4 = fold32_16(row16_sum_u32(acc));
-    if ((((uintptr_t)dst + (uintptr_t)cs) & 1u) == 0) t_l4 = bswap16(t_l4);
-    const uint32_t l4c = (~fold32_16(t_l4 + proto + tlen)) & 0xFFFFu;
-    if (r < hk) {
-      if (v4) put_be16(hv, x0h, 10, (~t_ip) & 0xFFFFu, hdr_len);
-      put_be16(hv, x0h, csum_at, l4c, hdr_len);
-      store_chunk(dbase + 16 * r, hv, x0h, pkt_len);
-    }
+  } else {
+    decoded_rows<U, NT>(vb, jlen, job.flags, room, max_segs, i, blockIdx.y == 0, &count[jb], &status[jb],
+                        out + obase + offset, dst, &sizes[slot0]);
   }
-  if (r == 0) sizes[slot0 + (uint32_t)i] = pkt_len;
 }
 
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs, uint8_t* out,
@@ -931,7 +986,7 @@ hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs
   if (!outpos) room = out_stride > offset ? out_stride - offset : 0;
   const uint32_t gy = (max_segs + 15) / 16;  // 16 segments (4 waves) per block
   if (gy > 65535u) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gso_rows_kernel<6, true>), dim3(n_jobs, gy), dim3(256), 0, s, arena, jobs, max_segs, out,
+  hipLaunchKernelGGL((gso_rows_kernel<WGCS_GSO_U, true>), dim3(n_jobs, gy), dim3(256), 0, s, arena, jobs, max_segs, out,
                      out_stride, outpos, offset, room, sizes, count, status);
   return hipGetLastError();
 }
