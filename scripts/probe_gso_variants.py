@@ -22,6 +22,9 @@ with the experiment, the outputs are kept in profiles/r2_probe_gso_*.jsonl):
                      (now the product tunable WGCS_GSO_WAVES, default 5)
   WGCS_P_BUF=0/1     payload windows through flat global loads (page test per
                      window) or raw buffer loads over the job's bytes (range check)
+  WGCS_P_PRIO=n      s_setprio(n) once a row's payload loads are issued
+  WGCS_P_DEADEXIT=1  segment groups past the job's last segment (bounded from
+                     the virtio header alone) retire before the verdict
   WGCS_P_EARLY=0/1   first payload batch issued before (1) or after (0) the
                      data-offset check (the decoded path is an out-of-line call)
   WGCS_P_A16=0/1     payload windows dword-aligned (alignbyte + 1 DPP dword) or
@@ -43,11 +46,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUTDIR = os.path.join(ROOT, "scripts", "probe_so")
 VARIANTS = {
-    "head": None,  # the committed kernel, built from `git archive HEAD` (see build())
     "w5": ["WGCS_GSO_WAVES=5"],
-    "w5_u8": ["WGCS_GSO_WAVES=5", "WGCS_GSO_U=8"],
-    "w5_u4": ["WGCS_GSO_WAVES=5", "WGCS_GSO_U=4"],
-    "w4": ["WGCS_GSO_WAVES=4"],
+    "w5_deadexit": ["WGCS_GSO_WAVES=5", "WGCS_P_DEADEXIT=1"],
 }
 
 
@@ -84,6 +84,7 @@ def main():
         _lib.LIB_PATH = os.path.join(OUTDIR, f"libwgcsum_{k}.so")
         devs[k] = Device(0)
     n_jobs, total, gso, max_segs, stride, offset = 256, 65535, 1460, 64, 1536, 16
+    max_segs = int(os.environ.get("WGCS_PROBE_MAX_SEGS", max_segs))  # output slots per job (45 used)
     pkts = [synth.make_super_packet(total, gso, seed=synth.SEED + k) for k in range(n_jobs)]
     jlen = len(pkts[0])
     arena = np.frombuffer(b"".join(pkts) + bytes(64), dtype=np.uint8).copy()

@@ -918,6 +918,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   const int nfull_s = clean_s ? (plen_s - hdr_s + gso_s - 1) / gso_s : 0;
   const int nseg_s = min(nfull_s, (int)max_segs);
   const bool live_s = clean_s && i < nseg_s;  // row-uniform
+  // A block past the job's last segment under every verdict retires now
+  // (callers size bufs for the largest read, conn.IdealBatchSize = 128
+  // slots, so most groups of a 64-KiB read are empty).  Group 0 always stays:
+  // it writes count / status and the GSO_NONE packet.  hdrLen >= csumStart +
+  // 20 (TCP, tun.go:608-613) or = csumStart + 8 (UDP) or the virtio value
+  // (raw jobs) bounds the segment count from above.
+  if (blockIdx.y > 0 && jlen >= 14) {
+    const int hmin = raw ? (int)hl : (tcp_s ? cs_s + 20 : cs_s + 8);
+    const bool split_type = ok_s && cs_s + 60 <= 0xFFFF;
+    const int nbound = !split_type ? INT32_MAX : (plen_s > hmin ? (plen_s - hmin + gso_s - 1) / gso_s : 0);
+    if ((!raw && t1 == GSO_NONE) || (split_type && segb >= nbound)) return;
+  }
 
   uint4 Q = funnel(H0, H1, hph);  // readBuf[16r, 16r + 16) (bytes below hdrLen)
   // the TCP data offset decides hdrLen (tun.go:601-614): block-uniform verdict
