@@ -46,8 +46,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUTDIR = os.path.join(ROOT, "scripts", "probe_so")
 VARIANTS = {
-    "w5": ["WGCS_GSO_WAVES=5"],
-    "w5_deadexit": ["WGCS_GSO_WAVES=5", "WGCS_P_DEADEXIT=1"],
+    "head": None,  # the committed kernel, built from `git archive HEAD` (see build())
+    "late": ["WGCS_P_EARLY=0"],
+    "early": ["WGCS_P_EARLY=1"],
 }
 
 
