@@ -25,6 +25,7 @@ with the experiment, the outputs are kept in profiles/r2_probe_gso_*.jsonl):
   WGCS_P_PRIO=n      s_setprio(n) once a row's payload loads are issued
   WGCS_P_DEADEXIT=1  segment groups past the job's last segment (bounded from
                      the virtio header alone) retire before the verdict
+  WGCS_P_HBUF=1      the header chunks through raw buffer loads too
   WGCS_P_EARLY=0/1   first payload batch issued before (1) or after (0) the
                      data-offset check (the decoded path is an out-of-line call)
   WGCS_P_A16=0/1     payload windows dword-aligned (alignbyte + 1 DPP dword) or
@@ -47,8 +48,8 @@ sys.path.insert(0, ROOT)
 OUTDIR = os.path.join(ROOT, "scripts", "probe_so")
 VARIANTS = {
     "head": None,  # the committed kernel, built from `git archive HEAD` (see build())
-    "late": ["WGCS_P_EARLY=0"],
-    "early": ["WGCS_P_EARLY=1"],
+    "hbuf": ["WGCS_P_HBUF=1"],
+    "hbuf_w6": ["WGCS_P_HBUF=1", "WGCS_GSO_WAVES=6"],
 }
 
 

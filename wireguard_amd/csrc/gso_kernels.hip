@@ -872,15 +872,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   const uint4 z = make_uint4(0, 0, 0, 0);
 
   // ---- header chunks in packet coordinates (lane r of each row: the 16-byte
-  // aligned chunks r and r + 1 from readBuf's), issued first: they need only
-  // the descriptor, and the data-offset check below waits for them without
-  // waiting for the payload loads.  Chunks past the packet's first 256 bytes
-  // (never header bytes on the rows' path) read the chunk holding readBuf[0].
+  // aligned chunks r and r + 1 from the one holding readBuf[0]), issued first:
+  // they need only the descriptor.  Raw buffer loads over the job's bytes:
+  // chunks past the job read as zeros.
   const int hph = (int)((uintptr_t)rb & 15u);
-  const uint8_t* hab = rb - hph + 16 * r;
-  const uint8_t* hend_s = rb + min(jlen > 10 ? (int)jlen - 10 : 0, kMaxHdrLen + 16);
-  uint4 H0 = ld16(hab < hend_s ? hab : rb - hph);
-  uint4 H1 = ld16(hab + 16 < hend_s ? hab + 16 : rb - hph);
+  const uint8_t* hbase = rb - hph;
+  const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(hbase), (short)0, (int)(jlen + 3u) - (int)(hbase - vb), 0x00020000);
+  uint4 H0 = bld16<false>(hrs, 16 * r);
+  uint4 H1 = bld16<false>(hrs, 16 * r + 16);
 
   // ---- virtio header + the IP version byte: 16 bytes from the dword below
   // vb, one scalar load (readable: jlen >= 14 and the arena contract)
