@@ -83,6 +83,39 @@ __global__ __launch_bounds__(256) void probe_copy(const uint8_t* __restrict__ sr
         }
       }
     }
+  } else if (MODE == 3) {
+    // aligned 16-byte loads, staged through LDS, read back at the byte phase
+    // (ds_read_b128 at any byte address: unaligned LDS access mode)
+    __shared__ uint4 stage[16][16 * U + 1];  // per row: its 16U+1 aligned chunks
+    const int row = threadIdx.x >> 4;
+    const int s = (int)((uintptr_t)s0 & 15);
+    const uint8_t* ab = s0 - s;
+    const uint8_t* hi = s0 + seg;
+    uint8_t* lrow = reinterpret_cast<uint8_t*>(&stage[row][0]);
+    for (int k0 = 0; k0 < nk; k0 += 16 * U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint8_t* ca = ab + 16 * (k0 + r + 16 * u);
+        stage[row][r + 16 * u] = ca < hi ? *reinterpret_cast<const uint4*>(ca) : make_uint4(0, 0, 0, 0);
+      }
+      if (r == 0) {
+        const uint8_t* ce = ab + 16 * (k0 + 16 * U);
+        stage[row][16 * U] = ce < hi ? *reinterpret_cast<const uint4*>(ce) : make_uint4(0, 0, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + r + 16 * u;
+        if (k < nk) {
+          uint4 v;
+          __builtin_memcpy(&v, lrow + 16 * (r + 16 * u) + s, 16);
+          *reinterpret_cast<uint4*>(d0 + 16 * k) = v;
+          acc += v.x ^ v.w;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
   } else {
     const int s = (int)((uintptr_t)s0 & 15);
     const uint8_t* ab = s0 - s;
@@ -120,7 +153,10 @@ __global__ __launch_bounds__(256) void probe_copy(const uint8_t* __restrict__ sr
 extern "C" int probe_copy_launch(const void* src, void* dst, uint32_t nseg, uint32_t seg, uint32_t stride, int mode,
                                  void* sink, void* stream) {
   const dim3 grid((nseg + 15) / 16);
-  if (mode == 2)
+  if (mode == 3)
+    hipLaunchKernelGGL((probe_copy<6, 3>), grid, dim3(256), 0, (hipStream_t)stream, (const uint8_t*)src,
+                       (uint8_t*)dst, nseg, seg, stride, (uint32_t*)sink);
+  else if (mode == 2)
     hipLaunchKernelGGL((probe_copy<6, 2>), grid, dim3(256), 0, (hipStream_t)stream, (const uint8_t*)src,
                        (uint8_t*)dst, nseg, seg, stride, (uint32_t*)sink);
   else if (mode == 0)

@@ -15,16 +15,16 @@ src = [torch.randint(0, 255, (nseg * seg + 4096,), dtype=torch.uint8, device="cu
 dst = [torch.empty(nseg * stride, dtype=torch.uint8, device="cuda") for _ in range(R)]
 sink = torch.zeros(16, dtype=torch.int32, device="cuda")
 st = torch.cuda.Stream()
-for mode in (0, 1, 2):
+for mode in (0, 1, 2, 3):
     for mis in (0, 1, 6):
         def go(k):
             L.probe_copy_launch(src[k % R].data_ptr() + mis, dst[k % R].data_ptr(), nseg, seg, stride, mode,
                                 sink.data_ptr(), st.cuda_stream)
         for k in range(10):
             go(k)
-        if mis == 1:
+        if mis in (1, 6):
             torch.cuda.synchronize()
-            a = src[0][1:1 + seg].cpu(); b = dst[0][:seg].cpu()
+            a = src[0][mis:mis + seg].cpu(); b = dst[0][:seg].cpu()
             ok = bool(torch.equal(a, b))
         else:
             ok = None
@@ -36,5 +36,5 @@ for mode in (0, 1, 2):
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / 200
         nb = 2 * nseg * seg
-        print(json.dumps({"mode": ["unaligned", "funnel", "dword-aligned+alignbyte"][mode], "misalign": mis, "us": round(us, 2),
+        print(json.dumps({"mode": ["unaligned", "funnel", "dword-aligned+alignbyte", "aligned+LDS byte-phase read"][mode], "misalign": mis, "us": round(us, 2),
                           "GBps_rw": round(nb / us / 1e3, 1), "check": ok}), flush=True)

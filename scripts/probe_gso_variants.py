@@ -48,8 +48,7 @@ sys.path.insert(0, ROOT)
 OUTDIR = os.path.join(ROOT, "scripts", "probe_so")
 VARIANTS = {
     "head": None,  # the committed kernel, built from `git archive HEAD` (see build())
-    "hbuf": ["WGCS_P_HBUF=1"],
-    "hbuf_w6": ["WGCS_P_HBUF=1", "WGCS_GSO_WAVES=6"],
+    "store_dw": [],  # store_chunk pieces picked by dword selects (no 128-bit shifts)
 }
 
 

@@ -66,9 +66,20 @@ __device__ __forceinline__ uint64_t chunk_sum(const uint4& v, int x0, int lo, in
          (v.z & expand_nibble((m16 >> 8) & 0xF)) + (v.w & expand_nibble((m16 >> 12) & 0xF));
 }
 
+// Dword i (0..3) of a chunk: bit-field selects (v_bfi), no 128-bit shifts --
+// and no ternaries on the components, which the compiler may turn into an
+// indexed private array promoted to LDS.
+__device__ __forceinline__ uint32_t dword_at(const uint4& v, int i) {
+  const uint32_t m1 = 0u - ((uint32_t)i & 1u), m2 = 0u - (((uint32_t)i >> 1) & 1u);
+  const uint32_t a = (v.y & m1) | (v.x & ~m1), b = (v.w & m1) | (v.z & ~m1);
+  return (b & m2) | (a & ~m2);
+}
+
 // Store the part of a destination chunk that lies in [0, pkt_len): full
 // chunks as one dwordx4; a partial chunk [lo, hi) as naturally aligned
 // byte/short/dword/dwordx2 pieces (at most 7 stores instead of 16 bytes).
+// Each piece's value is picked by dword selects: every piece lies inside one
+// dword, or is the aligned dword pair (0,1) / (2,3).
 __device__ __forceinline__ void store_chunk(uint8_t* dchunk, const uint4& v, int x0, int pkt_len) {
   if (x0 >= 0 && x0 + 16 <= pkt_len) {
     *reinterpret_cast<uint4*>(dchunk) = v;
@@ -77,19 +88,18 @@ __device__ __forceinline__ void store_chunk(uint8_t* dchunk, const uint4& v, int
   int p = max(-x0, 0);
   const int hi = min(pkt_len - x0, 16);
   if (p >= hi) return;
-  const u128 t = to128(v);
-  auto at = [&](int q) { return (uint64_t)(t >> (8 * q)); };  // bytes [q, q + 8)
-  if ((p & 1) && p < hi) { dchunk[p] = (uint8_t)at(p); p += 1; }
-  if ((p & 2) && p + 2 <= hi) { *reinterpret_cast<uint16_t*>(dchunk + p) = (uint16_t)at(p); p += 2; }
-  if ((p & 4) && p + 4 <= hi) { *reinterpret_cast<uint32_t*>(dchunk + p) = (uint32_t)at(p); p += 4; }
+  auto b8 = [&](int q) { return (uint8_t)(dword_at(v, q >> 2) >> (8 * (q & 3))); };
+  auto b16 = [&](int q) { return (uint16_t)(dword_at(v, q >> 2) >> (8 * (q & 2))); };  // q even
+  if ((p & 1) && p < hi) { dchunk[p] = b8(p); p += 1; }
+  if ((p & 2) && p + 2 <= hi) { *reinterpret_cast<uint16_t*>(dchunk + p) = b16(p); p += 2; }
+  if ((p & 4) && p + 4 <= hi) { *reinterpret_cast<uint32_t*>(dchunk + p) = dword_at(v, p >> 2); p += 4; }
   if (p + 8 <= hi) {  // p is 0 or 8 here
-    const uint64_t q = at(p);
-    *reinterpret_cast<uint2*>(dchunk + p) = make_uint2((uint32_t)q, (uint32_t)(q >> 32));
+    *reinterpret_cast<uint2*>(dchunk + p) = p ? make_uint2(v.z, v.w) : make_uint2(v.x, v.y);
     p += 8;
   }
-  if (p + 4 <= hi) { *reinterpret_cast<uint32_t*>(dchunk + p) = (uint32_t)at(p); p += 4; }
-  if (p + 2 <= hi) { *reinterpret_cast<uint16_t*>(dchunk + p) = (uint16_t)at(p); p += 2; }
-  if (p < hi) dchunk[p] = (uint8_t)at(p);
+  if (p + 4 <= hi) { *reinterpret_cast<uint32_t*>(dchunk + p) = dword_at(v, p >> 2); p += 4; }
+  if (p + 2 <= hi) { *reinterpret_cast<uint16_t*>(dchunk + p) = b16(p); p += 2; }
+  if (p < hi) dchunk[p] = b8(p);
 }
 
 template <bool SUM>
