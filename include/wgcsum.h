@@ -265,16 +265,16 @@ int wgcs_stager_copy_out(wgcs_stager *st, uint64_t batch, int read_idx, uint8_t 
 /* ---- Tun.Write batch staging (tun/tun.go:654-700) ----
  * A ring of `depth` slots; a slot aggregates up to max_writes Tun.Write calls
  * (<= max_pkts packets and <= max_bytes packet bytes in all).
- * wgcs_wstager_push stages one Write call -- bufs[i][offset:lens[i]], the
- * packets as device/receive.go:483 slices them, caps[i] = cap(bufs[i]) -- into
- * pinned memory and plans its flows on the host assuming valid checksums.
+ * wgcs_wstager_push stages one Write call (n <= WGCS_GRO_MAX_CALL buffers) --
+ * bufs[i][offset-10:lens[i]], the packets as device/receive.go:483 slices
+ * them, caps[i] = cap(bufs[i]) -- into pinned memory; no host planning.
  * wgcs_wstager_submit queues, on the slot's own stream, one H2D of every staged
- * packet, ONE checksumValid (VALIDATE) launch over every GRO candidate of every
- * staged call, ONE coalesce launch over every merged super-packet, and the D2H
- * of both.  wgcs_wstager_wait settles the slot: a call whose plan used a
- * checksum found invalid is re-planned with the real bits (one more small
- * round trip for that call only), so results are exactly handleGRO's
- * (gro.go:1326-1367).  wgcs_wstager_result hands back, per call, what
+ * packet, ONE device-resident handleGRO launch over every staged call (the
+ * kernel of wgcs_handle_gro_batch: flow tables, checksumValid, coalescing and
+ * apply* per call, on Go-sized slices in HBM), a gather of every call's
+ * toWrite images and one D2H, so results are exactly handleGRO's
+ * (gro.go:1326-1367).  wgcs_wstager_wait waits for the slot.
+ * wgcs_wstager_result hands back, per call, what
  * Tun.Write passes to write(2) (tun.go:687-698): to_write[k] = handleGRO's
  * toWrite and pkts[k][0:pkt_lens[k]] = bufs[to_write[k]][offset-10:] after
  * handleGRO (10-byte virtio header + packet) in pinned memory, valid until the

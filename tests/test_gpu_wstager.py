@@ -1,9 +1,9 @@
 """GPU parity: the Tun.Write stager (wgcs_wstager_*) vs the oracle's
 handleGRO per Write call -- status, toWrite and every byte Tun.Write hands to
 write(2) (bufs[i][offset-10:len] for i in toWrite, tun/tun.go:687-698), for
-many calls batched into one VALIDATE + one coalesce launch, including calls
-whose speculative plan must be redone (invalid checksums), prepends, capacity
-limits, UDP GRO off, and an invalid offset."""
+many calls batched into one device handleGRO launch (one workgroup per call),
+including invalid checksums, prepends, capacity limits, UDP GRO off, an
+invalid offset, offsets other than 16 and Write calls with no buffers."""
 import numpy as np
 import pytest
 
@@ -123,4 +123,50 @@ def test_write_stager_ring_reuse(dev):
             err, tw_p, writes_p = ws.result(b, idx, len(pkts))
             assert (0 if err is None else err.code, tw_p) == (rc, tw)
             assert writes_p == writes, _first_diff(writes_p, writes)
+    ws.close()
+
+
+@pytest.mark.parametrize("offset", [10, 13, 16, 40])
+def test_write_stager_offsets(dev, offset):
+    """Tun.Write offsets below and above the 16-byte headroom (the device slices
+    put every packet on a 16-byte boundary whatever the offset), and an empty
+    Write call between two real ones."""
+    calls = _calls(4 + offset)[:6]
+    ws = WriteStager(dev, depth=2, max_writes=8, max_pkts=8 * 128, max_bytes=8 * 128 * 1600)
+    idxs = []
+    for k, (pkts, cap, can_udp, lo) in enumerate(calls):
+        if lo:  # the invalid-offset override is for OFFSET 16
+            lo = {i: offset for i in lo}
+        capk = cap if isinstance(cap, int) else (lambda n, c=cap: c(n) - OFFSET + offset)
+        bufs, lens = _mk(pkts, capk, offset, lo)
+        idxs.append(ws.push(bufs, lens, offset, can_udp))
+        if k == 2:
+            idxs.append(ws.push([], [], offset, True))
+    b = ws.submit()
+    ws.wait(b)
+    j = 0
+    for k, (pkts, cap, can_udp, lo) in enumerate(calls):
+        if lo:
+            lo = {i: offset for i in lo}
+        capk = cap if isinstance(cap, int) else (lambda n, c=cap: c(n) - OFFSET + offset)
+        rc, tw, writes = _oracle_writes(pkts, capk, can_udp, offset, lo)
+        err, tw_p, writes_p = ws.result(b, idxs[j], len(pkts))
+        assert (0 if err is None else err.code, tw_p) == (rc, tw), k
+        assert writes_p == writes, f"call {k}: {_first_diff(writes_p, writes)}"
+        j += 1
+        if k == 2:
+            err, tw_p, writes_p = ws.result(b, idxs[j], 0)
+            assert err is None and tw_p == [] and writes_p == []
+            j += 1
+    ws.close()
+
+
+def test_write_stager_rejects_oversized_call(dev):
+    """A Write call holds at most conn.BatchSize (128) buffers (WGCS_GRO_MAX_CALL)."""
+    ws = WriteStager(dev, depth=2, max_writes=4, max_pkts=512, max_bytes=512 * 1600)
+    pkts = [p for _ in range(5) for p in flow(26, seed=7)][:129]
+    bufs, lens = _mk(pkts)
+    with pytest.raises(Exception) as ei:
+        ws.push(bufs, lens, OFFSET, True)
+    assert getattr(ei.value, "code", None) == -1, ei.value
     ws.close()

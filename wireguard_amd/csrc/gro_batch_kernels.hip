@@ -673,6 +673,95 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
   }
 }
 
+// ---- write stager (wstager.cpp): staged packets -> slices, toWrite images -> packed output
+//
+// One wave per staged packet: its 16 bytes of headroom (virtio header) and
+// packet, aligned 16-byte chunks from the packed stage into its slice.
+__global__ __launch_bounds__(256) void ws_scatter_kernel(const uint8_t* __restrict__ stage,
+                                                         uint8_t* __restrict__ arena, const WsMove* __restrict__ mv,
+                                                         uint32_t n) {
+  const uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  if (w >= n) return;  // wave-uniform
+  const WsMove m = mv[w];
+  const uint4* s = reinterpret_cast<const uint4*>(stage + m.src);
+  uint4* d = reinterpret_cast<uint4*>(arena + m.dst);
+  uint32_t k = lane;
+  for (; k + 64 < m.n16; k += 128) {  // two chunks per lane in flight
+    const uint4 a = s[k], b = s[k + 64];
+    d[k] = a;
+    d[k + 64] = b;
+  }
+  if (k < m.n16) d[k] = s[k];
+}
+
+// One block per call: Tun.Write's write(2) images, bufs[i][offset-10:len] for
+// i in toWrite (tun.go:687-698), packed in toWrite order into the call's
+// output region; entry k takes 16 + align16(len - offset) bytes starting with
+// the aligned chunk that holds the virtio header, so its image starts 6 bytes
+// in.  wlen[first + k] = its length.  An image set larger than the region
+// (not possible: each packet's bytes end up in at most one written buffer)
+// would be reported as WGCS_ERR_OUT_OF_RANGE, never written past it.
+__global__ __launch_bounds__(256) void ws_gather_kernel(const uint8_t* __restrict__ arena,
+                                                        const wgcs_gro_buf* __restrict__ bufs,
+                                                        const wgcs_gro_call* __restrict__ calls,
+                                                        const WsOut* __restrict__ outs, int32_t* __restrict__ status,
+                                                        const int32_t* __restrict__ n_write,
+                                                        const int32_t* __restrict__ to_write,
+                                                        int32_t* __restrict__ wlen, uint8_t* __restrict__ out) {
+  __shared__ uint32_t pos[kMaxB + 1];
+  __shared__ uint64_t src[kMaxB];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const wgcs_gro_call call = calls[blockIdx.x];
+  const WsOut o = outs[blockIdx.x];
+  const int st = status[blockIdx.x];
+  int nw = st == 0 ? n_write[blockIdx.x] : 0;
+  nw = nw < 0 ? 0 : (nw > kMaxB ? kMaxB : nw);
+  if (t < nw) {
+    const int i = to_write[call.first + t];
+    const wgcs_gro_buf b = bufs[call.first + i];
+    const uint32_t pl = b.len - (uint32_t)call.offset;
+    wlen[call.first + t] = (int32_t)(pl + kVnet);
+    pos[t + 1] = 16u + ((pl + 15u) & ~15u);
+    src[t] = b.off + (uint64_t)call.offset - 16u;
+  }
+  __syncthreads();
+  if (t == 0) {
+    pos[0] = 0;
+    for (int k = 1; k <= nw; ++k) pos[k] += pos[k - 1];
+    if (pos[nw] > o.room) status[blockIdx.x] = WGCS_ERR_OUT_OF_RANGE;
+  }
+  __syncthreads();
+  if (pos[nw] > o.room) return;  // block-uniform
+  for (int k = wv; k < nw; k += 4) {  // wave-uniform: one image per wave
+    const uint4* s = reinterpret_cast<const uint4*>(arena + src[k]);
+    uint4* d = reinterpret_cast<uint4*>(out + o.base + pos[k]);
+    const uint32_t n16 = (pos[k + 1] - pos[k]) >> 4;
+    uint32_t c = (uint32_t)lane;
+    for (; c + 64 < n16; c += 128) {
+      const uint4 a = s[c], b = s[c + 64];
+      d[c] = a;
+      d[c + 64] = b;
+    }
+    if (c < n16) d[c] = s[c];
+  }
+}
+
+hipError_t launch_ws_scatter(const uint8_t* stage, uint8_t* arena, const WsMove* mv, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(ws_scatter_kernel, dim3((n + 3) / 4), dim3(256), 0, s, stage, arena, mv, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_ws_gather(const uint8_t* arena, const wgcs_gro_buf* bufs, const wgcs_gro_call* calls,
+                            const WsOut* outs, uint32_t n_calls, int32_t* status, const int32_t* n_write,
+                            const int32_t* to_write, int32_t* wlen, uint8_t* out, hipStream_t s) {
+  if (n_calls == 0) return hipSuccess;
+  hipLaunchKernelGGL(ws_gather_kernel, dim3(n_calls), dim3(256), 0, s, arena, bufs, calls, outs, status, n_write,
+                     to_write, wlen, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_gro_batch(uint8_t* arena, wgcs_gro_buf* bufs, const wgcs_gro_call* calls, uint32_t n_calls,
                             int32_t* status, int32_t* n_write, int32_t* to_write, hipStream_t s) {
   if (n_calls == 0) return hipSuccess;

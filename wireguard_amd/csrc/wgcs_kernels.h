@@ -109,6 +109,24 @@ enum : uint8_t { GRO_KIND_V6 = 1, GRO_KIND_UDP = 2, GRO_KIND_PSH = 4, GRO_KIND_R
 hipError_t launch_gro_batch(uint8_t* arena, wgcs_gro_buf* bufs, const wgcs_gro_call* calls, uint32_t n_calls,
                             int32_t* status, int32_t* n_write, int32_t* to_write, hipStream_t s);
 
+// Write stager around the batched handleGRO (wstager.cpp): packets staged
+// back to back are moved into their Go-sized slices of the device arena, and
+// after the handleGRO launch the toWrite images of each call are packed into
+// that call's output region.  Both copies are 16-byte aligned on both sides.
+struct WsMove {
+  uint64_t src, dst;  // 16-byte aligned stage / arena offsets
+  uint32_t n16, pad;  // 16-byte chunks
+};
+struct WsOut {
+  uint64_t base;  // the call's output region (16-byte aligned)
+  uint32_t room;  // its size in bytes
+  uint32_t pad;
+};
+hipError_t launch_ws_scatter(const uint8_t* stage, uint8_t* arena, const WsMove* mv, uint32_t n, hipStream_t s);
+hipError_t launch_ws_gather(const uint8_t* arena, const wgcs_gro_buf* bufs, const wgcs_gro_call* calls,
+                            const WsOut* outs, uint32_t n_calls, int32_t* status, const int32_t* n_write,
+                            const int32_t* to_write, int32_t* wlen, uint8_t* out, hipStream_t s);
+
 hipError_t launch_gro_coalesce(const uint8_t* stage, const GroItem* items, uint32_t n_items, const GroSeg* segs,
                                uint32_t n_segs, uint8_t* out, hipStream_t s);
 

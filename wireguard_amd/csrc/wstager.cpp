@@ -5,18 +5,19 @@
 // toWrite entry of bufs[i][offset-10:] (tun.go:687-698); it is called from
 // every peer's RoutineSendToInternet (device/receive.go:483-498).  One such
 // call is far too small for a GPU round trip (wgcs_handle_gro: ~70 us), so the
-// write stager aggregates many Write batches into one pinned ring slot:
+// write stager aggregates many Write calls into one pinned ring slot and runs
+// all of handleGRO on the GPU, one workgroup per call (gro_batch_kernels.hip):
 //
-//   push      stage one Write call's packets (pinned), plan its flows on the
-//             host assuming every checksum is valid (wgcs_gro_plan.h)
-//   submit    slot stream: H2D of all staged packets + candidate descriptors
-//             -> ONE VALIDATE launch over every candidate of every batch
-//             -> ONE coalesce launch over every merged item of every batch
-//             -> D2H of the validity bits and the super-packets
-//   wait      settle each batch: a batch whose plan consulted a checksum that
-//             is invalid is re-planned with the real bits and its items rebuilt
-//             (one more small round trip, that batch only)
-//   result    per batch, what Tun.Write hands to write(2): for each toWrite
+//   push      copy one Write call's packets into the pinned slot, back to back
+//             (16 B of headroom before each holds the caller's
+//             bufs[i][offset-10:offset]); record each as a Go slice of the
+//             caller's capacity in the slot's device arena.  No host planning.
+//   submit    slot stream: H2D of the packets and descriptors -> scatter into
+//             the slices -> ONE handleGRO launch over every call (flow table,
+//             checksumValid, coalescing, apply*, all on the device) -> gather
+//             every call's toWrite images into its output region -> one D2H
+//   wait      the slot's event
+//   result    per call, what Tun.Write hands to write(2): for each toWrite
 //             index the bytes bufs[i][offset-10:len(bufs[i])] after handleGRO,
 //             in pinned memory (a 10-byte virtio header + packet)
 //
@@ -24,6 +25,12 @@
 // k+1's kernels and slot k+2's H2D.  The caller's buffers are only read by
 // push; handleGRO's in-place edits of bufs are not replayed into them (Write's
 // callers recycle bufs after the call, device/receive.go:500-505).
+//
+// Device arena layout of one staged buffer (16-byte aligned region): 16 B pad,
+// then the slice `off` chosen so that off + offset (the packet) is 16-byte
+// aligned, then cap - offset bytes of slice, 16 B pad.  The scatter copies the
+// headroom chunk + packet as whole aligned chunks; the gather copies the
+// aligned chunk holding the virtio header + the packet as whole chunks.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,59 +41,57 @@
 
 #include "../../include/wgcsum.h"
 #include "wgcs_ctx.h"
-#include "wgcs_gro_plan.h"
 #include "wgcs_kernels.h"
 
 using namespace wgcs;
-using namespace wgcs::gro;
 
 namespace {
 
 constexpr size_t kHead = 16;  // headroom before each staged packet: its virtio header bytes go there
+constexpr int kVnet = 10;     // virtioNetHdrLen (tun/gro.go:67)
 
 inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-struct WBatch {  // one Tun.Write call
-  int n = 0, offset = 0, can_udp = 0;
-  int status = 0;                  // 0 or WGCS_ERR_INVALID_OFFSET (gro.go:1335-1337)
-  int n_eff = 0;                   // packets the handleGRO loop reaches
-  std::vector<uint64_t> stage;     // staged packet offsets (packet k's bytes at h_stage + stage[k])
-  std::vector<size_t> lens0, caps0;
-  std::vector<int> cand;
-  std::vector<uint32_t> vidx;      // candidate k -> index into the slot's validity array
-  std::vector<uint8_t> consulted;  // validity bits the plan depended on
-  Plan plan;
-  std::vector<int> order;          // order[i] = original buffer now at position i
-  std::vector<size_t> lens;        // final len(bufs[i])
-  bool fixup = false;              // items rebuilt by the settle pass (outputs in the fixup region)
+struct WCall {  // one Tun.Write call
+  int n = 0, offset = 0;
+  int status = 0;   // 0 or WGCS_ERR_INVALID_OFFSET (gro.go:1335-1337) before the launch
+  int dev = -1;     // index among the slot's device calls (-1: nothing staged)
+  uint32_t first = 0;
+  uint64_t base = 0;  // its output region in h_out (= its staged bytes)
 };
 
 struct WSlot {
   uint64_t id = 0;
-  int state = 0;  // 0 free, 1 open, 2 submitted, 3 settled
-  std::vector<WBatch> batches;
-  size_t used = 0;       // staged bytes
-  uint64_t out_used = 0; // coalesce output bytes
-  uint32_t ncand = 0;
-  std::vector<GroItem> items;
-  std::vector<GroSeg> segs;
+  int state = 0;  // 0 free, 1 open, 2 submitted, 3 done
+  std::vector<WCall> calls;
+  size_t used = 0;      // staged bytes (and output bytes)
+  uint64_t arena = 0;   // device arena bytes of the staged slices
+  uint32_t npk = 0, ndev = 0;
   // pinned host
   uint8_t* h_stage = nullptr;
-  wgcs_pkt* h_pkts = nullptr;
-  uint8_t* h_valid = nullptr;
-  uint8_t* h_meta = nullptr;  // items | segs (H2D)
+  wgcs_gro_buf* h_bufs = nullptr;
+  WsMove* h_moves = nullptr;
+  wgcs_gro_call* h_calls = nullptr;
+  WsOut* h_outs = nullptr;
+  int32_t* h_res = nullptr;  // status[ndev] | n_write[ndev] | to_write[npk] | wlen[npk]
   uint8_t* h_out = nullptr;
-  uint8_t* h_fix = nullptr;   // settle pass: rebuilt items' outputs
-  size_t fix_cap = 0;
   // device
   uint8_t* d_stage = nullptr;
-  wgcs_pkt* d_pkts = nullptr;
-  uint8_t* d_valid = nullptr;
-  uint8_t* d_meta = nullptr;
+  wgcs_gro_buf* d_bufs = nullptr;
+  WsMove* d_moves = nullptr;
+  wgcs_gro_call* d_calls = nullptr;
+  WsOut* d_outs = nullptr;
+  int32_t* d_res = nullptr;
   uint8_t* d_out = nullptr;
-  uint8_t* d_fix = nullptr;
+  uint8_t* d_arena = nullptr;
+  size_t arena_cap = 0;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
+
+  const int32_t* res_status() const { return h_res; }
+  const int32_t* res_nwrite() const { return h_res + ndev; }
+  const int32_t* res_towrite() const { return h_res + 2 * (size_t)ndev; }
+  const int32_t* res_wlen() const { return h_res + 2 * (size_t)ndev + npk; }
 };
 
 }  // namespace
@@ -94,7 +99,7 @@ struct WSlot {
 struct wgcs_wstager {
   wgcs_ctx* ctx = nullptr;
   uint32_t depth = 0, max_writes = 0, max_pkts = 0;
-  size_t max_bytes = 0, max_out = 0, max_meta = 0;
+  size_t max_bytes = 0;
   std::vector<WSlot> slots;
   uint32_t open = 0;
   uint64_t next_id = 1;
@@ -109,9 +114,11 @@ struct wgcs_wstager {
 namespace {
 
 void free_wslot(WSlot& s) {
-  for (void* p : {(void*)s.h_stage, (void*)s.h_pkts, (void*)s.h_valid, (void*)s.h_meta, (void*)s.h_out, (void*)s.h_fix})
+  for (void* p : {(void*)s.h_stage, (void*)s.h_bufs, (void*)s.h_moves, (void*)s.h_calls, (void*)s.h_outs,
+                  (void*)s.h_res, (void*)s.h_out})
     if (p) hipHostFree(p);
-  for (void* p : {(void*)s.d_stage, (void*)s.d_pkts, (void*)s.d_valid, (void*)s.d_meta, (void*)s.d_out, (void*)s.d_fix})
+  for (void* p : {(void*)s.d_stage, (void*)s.d_bufs, (void*)s.d_moves, (void*)s.d_calls, (void*)s.d_outs,
+                  (void*)s.d_res, (void*)s.d_out, (void*)s.d_arena})
     if (p) hipFree(p);
   if (s.done) hipEventDestroy(s.done);
   if (s.stream) hipStreamDestroy(s.stream);
@@ -126,47 +133,12 @@ int open_wslot(wgcs_wstager* ws, uint32_t idx) {
   }
   s.id = ws->next_id++;
   s.state = 1;
-  s.batches.clear();
+  s.calls.clear();
   s.used = 0;
-  s.out_used = 0;
-  s.ncand = 0;
-  s.items.clear();
-  s.segs.clear();
+  s.arena = 0;
+  s.npk = s.ndev = 0;
   ws->open = idx;
   return WGCS_OK;
-}
-
-// Plan batch b of slot s with the validity bits `valid` (per packet of the
-// batch): handleGRO's loop + apply, as a gather plan whose items write into
-// the output region at `out_base`.
-void plan_batch(WSlot& s, WBatch& b, const std::vector<uint8_t>& valid, uint64_t out_base) {
-  const int n = b.n;
-  std::vector<uint8_t*> ptrs(n);  // tokens: follow the prepend swaps (gro.go:696-697)
-  for (int i = 0; i < n; ++i) ptrs[i] = reinterpret_cast<uint8_t*>((uintptr_t)(i + 1));
-  b.lens = b.lens0;
-  std::vector<size_t> caps = b.caps0;
-  std::vector<const uint8_t*> orig(n, nullptr);
-  // orig[i] = the packet bytes (bufs[i][offset:]): staged at h_stage + stage[i]
-  for (int i = 0; i < b.n_eff; ++i) orig[i] = s.h_stage + b.stage[i];
-  Planner P;
-  init_planner(P, ptrs.data(), b.lens.data(), caps.data(), b.n_eff, b.offset, orig, valid);
-  b.plan = Plan();
-  b.plan.out_bytes = out_base;
-  make_plan(P, b.cand, b.stage, b.n_eff, b.status != 0, b.plan);
-  b.consulted = P.consulted;
-  b.order.resize(n);
-  for (int i = 0; i < n; ++i) b.order[i] = (int)((uintptr_t)ptrs[i] - 1);
-}
-
-// GroItem/GroSeg offsets are relative to the staged packets (head_off /
-// src_off are stage offsets; the packet's own bytes start at stage[k]).
-void add_plan_items(WSlot& s, WBatch& b) {
-  const uint32_t seg0 = (uint32_t)s.segs.size();
-  for (GroItem it : b.plan.items) {
-    it.seg_first += seg0;
-    s.items.push_back(it);
-  }
-  s.segs.insert(s.segs.end(), b.plan.segs.begin(), b.plan.segs.end());
 }
 
 }  // namespace
@@ -186,23 +158,25 @@ int wgcs_wstager_create(wgcs_ctx* ctx, uint32_t depth, uint32_t max_writes, uint
   ws->max_writes = max_writes;
   ws->max_pkts = max_pkts;
   ws->max_bytes = al16(max_bytes + (size_t)max_pkts * (kHead + 16));
-  // coalesced outputs never exceed the staged packets + one virtio header and alignment per packet
-  ws->max_out = al16(max_bytes + (size_t)max_pkts * 32);
-  ws->max_meta = (size_t)max_pkts * (sizeof(GroItem) + sizeof(GroSeg)) + 64;
   ws->slots.resize(depth);
   hipSetDevice(ctx->device);
+  const size_t nres = (2 * (size_t)max_writes + 2 * (size_t)max_pkts) * sizeof(int32_t);
   for (auto& s : ws->slots) {
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_stage, ws->max_bytes + 64, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_pkts, max_pkts * sizeof(wgcs_pkt), hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_valid, max_pkts + 64, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_meta, ws->max_meta, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_out, ws->max_out + 64, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_bufs, max_pkts * sizeof(wgcs_gro_buf), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_moves, max_pkts * sizeof(WsMove), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_calls, max_writes * sizeof(wgcs_gro_call), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_outs, max_writes * sizeof(WsOut), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_res, nres, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_out, ws->max_bytes + 64, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMalloc((void**)&s.d_stage, ws->max_bytes + 64);
-    if (e == hipSuccess) e = hipMalloc((void**)&s.d_pkts, max_pkts * sizeof(wgcs_pkt));
-    if (e == hipSuccess) e = hipMalloc((void**)&s.d_valid, max_pkts + 64);
-    if (e == hipSuccess) e = hipMalloc((void**)&s.d_meta, ws->max_meta);
-    if (e == hipSuccess) e = hipMalloc((void**)&s.d_out, ws->max_out + 64);
+    if (e == hipSuccess) e = hipMalloc((void**)&s.d_bufs, max_pkts * sizeof(wgcs_gro_buf));
+    if (e == hipSuccess) e = hipMalloc((void**)&s.d_moves, max_pkts * sizeof(WsMove));
+    if (e == hipSuccess) e = hipMalloc((void**)&s.d_calls, max_writes * sizeof(wgcs_gro_call));
+    if (e == hipSuccess) e = hipMalloc((void**)&s.d_outs, max_writes * sizeof(WsOut));
+    if (e == hipSuccess) e = hipMalloc((void**)&s.d_res, nres);
+    if (e == hipSuccess) e = hipMalloc((void**)&s.d_out, ws->max_bytes + 64);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -238,77 +212,73 @@ int wgcs_wstager_destroy(wgcs_wstager* ws) {
 int wgcs_wstager_push(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, const size_t* caps, int n,
                       int offset, int can_udp_gro, int* write_idx) {
   if (!ws || !write_idx || n < 0 || (n > 0 && (!bufs || !lens || !caps))) return WGCS_ERR_INVALID_ARG;
+  if (n > WGCS_GRO_MAX_CALL)
+    return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: %d buffers in one Write call (at most %d)", n,
+                   WGCS_GRO_MAX_CALL);
   std::lock_guard<std::mutex> g(ws->mu);
   WSlot& s = ws->slots[ws->open];
-  // handleGRO's loop stops at the first buffer with an invalid offset (gro.go:1335-1337)
-  int n_eff = n;
+  if (s.calls.size() >= ws->max_writes) return set_err(ws->ctx, WGCS_ERR_BATCH_FULL, "wstager: open batch is full");
+  WCall c;
+  c.n = n;
+  c.offset = offset;
+  // handleGRO's loop stops at the first buffer with an invalid offset
+  // (gro.go:1335-1337) and Tun.Write then returns (0, err) without writing
+  // anything (tun.go:667-676): nothing to stage
   for (int i = 0; i < n; ++i)
-    if (offset < kVnetLen || (long)offset > (long)lens[i] - 1) {
-      n_eff = i;
+    if (offset < kVnet || (long)offset > (long)lens[i] - 1) {
+      c.status = WGCS_ERR_INVALID_OFFSET;
       break;
     }
-  if (n_eff < n) {  // Tun.Write returns (0, err) and writes nothing (tun.go:667-676): no staging needed
-    if (s.batches.size() >= ws->max_writes)
-      return set_err(ws->ctx, WGCS_ERR_BATCH_FULL, "wstager: open batch is full");
-    WBatch b;
-    b.n = n;
-    b.offset = offset;
-    b.status = WGCS_ERR_INVALID_OFFSET;
-    *write_idx = (int)s.batches.size();
-    s.batches.push_back(std::move(b));
+  if (c.status || n == 0) {
+    *write_idx = (int)s.calls.size();
+    s.calls.push_back(c);
     return WGCS_OK;
   }
   size_t need = 0;
-  uint32_t npk = 0;
-  for (int i = 0; i < n_eff; ++i) {
-    if (lens[i] - (size_t)offset > 65535 + 64) return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: packet > 64 KiB");
+  uint64_t arena = 0;
+  for (int i = 0; i < n; ++i) {
+    if (caps[i] < lens[i] || caps[i] > 0xFFFFFFFFull)
+      return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: cap(bufs[%d]) < len or >= 4 GiB", i);
     need += kHead + al16(lens[i] - offset);
+    arena += 32 + al16((size_t)offset) + al16(caps[i] - offset);
   }
-  uint32_t npk_total = 0;
-  for (const auto& b : s.batches) npk_total += (uint32_t)b.n_eff;
-  npk = (uint32_t)n_eff;
-  if (s.batches.size() >= ws->max_writes || npk_total + npk > ws->max_pkts || s.used + need > ws->max_bytes)
+  if (s.npk + (uint32_t)n > ws->max_pkts || s.used + need > ws->max_bytes)
     return set_err(ws->ctx, WGCS_ERR_BATCH_FULL, "wstager: open batch is full");
-  WBatch b;
-  b.n = n;
-  b.offset = offset;
-  b.can_udp = can_udp_gro != 0;
-  b.n_eff = n_eff;
-  b.status = n_eff < n ? WGCS_ERR_INVALID_OFFSET : 0;
-  b.stage.assign(n, 0);
-  b.lens0.assign(lens, lens + n);
-  b.caps0.assign(caps, caps + n);
-  b.cand.assign(n, NOT_CAND);
-  std::vector<uint8_t> assume(n, 0);
-  for (int i = 0; i < n_eff; ++i) {
+  c.dev = (int)s.ndev;
+  c.first = s.npk;
+  c.base = s.used;
+  for (int i = 0; i < n; ++i) {
     const size_t pl = lens[i] - (size_t)offset;
-    const uint64_t at = s.used + kHead;
-    // headroom: the caller's bytes bufs[i][offset-10:offset].  A buffer whose
-    // table item was dropped (tcpGRO's deleteAt after coalesceItemInvalidChecksum,
-    // gro.go:942-945) is written with them, as no virtio header is ever encoded
-    // into it; NOOP and unmerged items get a zero header at settle (wait).
-    memset(s.h_stage + s.used, 0, kHead - kVnetLen);
-    memcpy(s.h_stage + at - kVnetLen, bufs[i] + offset - kVnetLen, kVnetLen);
+    const uint64_t at = s.used + kHead;  // the packet in the stage (16-byte aligned)
+    memset(s.h_stage + s.used, 0, kHead - kVnet);
+    memcpy(s.h_stage + at - kVnet, bufs[i] + offset - kVnet, kVnet);
     memcpy(s.h_stage + at, bufs[i] + offset, pl);
-    b.stage[i] = at;
     s.used = at + al16(pl);
-    b.cand[i] = gro_candidate(s.h_stage + at, pl, b.can_udp);
-    if (b.cand[i] != NOT_CAND) {
-      const bool v6 = b.cand[i] == TCP6 || b.cand[i] == UDP6;
-      const bool udp = b.cand[i] == UDP4 || b.cand[i] == UDP6;
-      wgcs_pkt_set(&s.h_pkts[s.ncand], at, (uint32_t)pl, (uint16_t)(v6 ? 40 : 20), 0, (uint8_t)(udp ? 17 : 6),
-                   (uint8_t)(v6 ? WGCS_PKT_V6 : 0));
-      b.vidx.push_back(s.ncand++);
-      assume[i] = 1;  // speculation: valid (checked at settle)
-    } else {
-      b.vidx.push_back(0xFFFFFFFFu);
-    }
+    const uint64_t pkt = s.arena + 16 + al16((size_t)offset);  // the packet in the arena (16-byte aligned)
+    wgcs_gro_buf& b = s.h_bufs[s.npk];
+    b.off = pkt - (uint64_t)offset;
+    b.len = (uint32_t)lens[i];
+    b.cap = (uint32_t)caps[i];
+    WsMove& m = s.h_moves[s.npk];
+    m.src = at - kHead;
+    m.dst = pkt - kHead;
+    m.n16 = (uint32_t)((kHead + al16(pl)) >> 4);
+    m.pad = 0;
+    s.arena += 32 + al16((size_t)offset) + al16(caps[i] - offset);
+    ++s.npk;
   }
-  plan_batch(s, b, assume, s.out_used);
-  s.out_used = b.plan.out_bytes;
-  add_plan_items(s, b);
-  *write_idx = (int)s.batches.size();
-  s.batches.push_back(std::move(b));
+  wgcs_gro_call& dc = s.h_calls[s.ndev];
+  dc.first = c.first;
+  dc.n = (uint32_t)n;
+  dc.offset = offset;
+  dc.flags = can_udp_gro ? WGCS_GRO_CAN_UDP : 0u;
+  WsOut& o = s.h_outs[s.ndev];
+  o.base = c.base;
+  o.room = (uint32_t)(s.used - c.base);
+  o.pad = 0;
+  ++s.ndev;
+  *write_idx = (int)s.calls.size();
+  s.calls.push_back(c);
   return WGCS_OK;
 }
 
@@ -319,25 +289,34 @@ int wgcs_wstager_submit(wgcs_wstager* ws, uint64_t* batch) {
   WSlot& s = ws->slots[ws->open];
   const hipStream_t q = s.stream;
   hipError_t e = hipSuccess;
-  const size_t ib = s.items.size() * sizeof(GroItem), sb = s.segs.size() * sizeof(GroSeg);
-  if (ib + sb > ws->max_meta || s.out_used > ws->max_out)
-    return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: plan larger than the slot");
-  if (s.used) e = hipMemcpyAsync(s.d_stage, s.h_stage, s.used, hipMemcpyHostToDevice, q);
-  if (e == hipSuccess && s.ncand) {
-    e = hipMemcpyAsync(s.d_pkts, s.h_pkts, s.ncand * sizeof(wgcs_pkt), hipMemcpyHostToDevice, q);
+  if (s.ndev) {
+    if (s.arena + 64 > s.arena_cap) {  // the slot is idle (open_wslot waited for it)
+      if (s.d_arena) hipFree(s.d_arena);
+      s.d_arena = nullptr;
+      s.arena_cap = 0;
+      const size_t want = al16(s.arena + s.arena / 4 + 64);
+      e = hipMalloc((void**)&s.d_arena, want);
+      if (e != hipSuccess) return hip_fail(ws->ctx, e, "wstager: device arena");
+      s.arena_cap = want;
+    }
+    const uint32_t nd = s.ndev, np = s.npk;
+    int32_t* d_status = s.d_res;
+    int32_t* d_nw = s.d_res + nd;
+    int32_t* d_tw = s.d_res + 2 * (size_t)nd;
+    int32_t* d_wlen = s.d_res + 2 * (size_t)nd + np;
+    e = hipMemcpyAsync(s.d_stage, s.h_stage, s.used, hipMemcpyHostToDevice, q);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.d_bufs, s.h_bufs, np * sizeof(wgcs_gro_buf), hipMemcpyHostToDevice, q);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.d_moves, s.h_moves, np * sizeof(WsMove), hipMemcpyHostToDevice, q);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.d_calls, s.h_calls, nd * sizeof(wgcs_gro_call), hipMemcpyHostToDevice, q);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.d_outs, s.h_outs, nd * sizeof(WsOut), hipMemcpyHostToDevice, q);
+    if (e == hipSuccess) e = launch_ws_scatter(s.d_stage, s.d_arena, s.d_moves, np, q);
+    if (e == hipSuccess) e = launch_gro_batch(s.d_arena, s.d_bufs, s.d_calls, nd, d_status, d_nw, d_tw, q);
     if (e == hipSuccess)
-      e = launch_checksum_batch(WGCS_MODE_VALIDATE, 0, s.d_stage, s.d_pkts, nullptr, s.ncand, s.d_valid, q,
-                                ws->ctx->num_cu, ws->ctx->tune);
-    if (e == hipSuccess) e = hipMemcpyAsync(s.h_valid, s.d_valid, s.ncand, hipMemcpyDeviceToHost, q);
-  }
-  if (e == hipSuccess && !s.items.empty()) {
-    memcpy(s.h_meta, s.items.data(), ib);
-    memcpy(s.h_meta + ib, s.segs.data(), sb);
-    e = hipMemcpyAsync(s.d_meta, s.h_meta, ib + sb, hipMemcpyHostToDevice, q);
+      e = launch_ws_gather(s.d_arena, s.d_bufs, s.d_calls, s.d_outs, nd, d_status, d_nw, d_tw, d_wlen, s.d_out, q);
     if (e == hipSuccess)
-      e = launch_gro_coalesce(s.d_stage, (const GroItem*)s.d_meta, (uint32_t)s.items.size(),
-                              (const GroSeg*)(s.d_meta + ib), (uint32_t)s.segs.size(), s.d_out, q);
-    if (e == hipSuccess) e = hipMemcpyAsync(s.h_out, s.d_out, s.out_used, hipMemcpyDeviceToHost, q);
+      e = hipMemcpyAsync(s.h_res, s.d_res, (2 * (size_t)nd + 2 * (size_t)np) * sizeof(int32_t), hipMemcpyDeviceToHost,
+                         q);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.h_out, s.d_out, s.used, hipMemcpyDeviceToHost, q);
   }
   if (e == hipSuccess) e = hipEventRecord(s.done, q);
   if (e != hipSuccess) return hip_fail(ws->ctx, e, "wstager submit");
@@ -346,9 +325,6 @@ int wgcs_wstager_submit(wgcs_wstager* ws, uint64_t* batch) {
   return open_wslot(ws, (ws->open + 1) % ws->depth);
 }
 
-// Wait for a submitted slot and settle it: batches whose plan consulted a
-// checksum that the VALIDATE kernel found invalid are re-planned with the real
-// bits; their rebuilt items go through the coalesce kernel once more.
 int wgcs_wstager_wait(wgcs_wstager* ws, uint64_t batch) {
   if (!ws) return WGCS_ERR_INVALID_ARG;
   hipEvent_t ev;
@@ -364,68 +340,11 @@ int wgcs_wstager_wait(wgcs_wstager* ws, uint64_t batch) {
   std::lock_guard<std::mutex> g(ws->mu);
   WSlot* s = ws->find(batch);
   if (!s) return WGCS_ERR_NOT_READY;
-  if (s->state == 3) return WGCS_OK;
-  std::vector<GroItem> fix_items;
-  std::vector<GroSeg> fix_segs;
-  uint64_t fix_out = 0;
-  for (WBatch& b : s->batches) {
-    if (b.status) continue;
-    bool redo = false;
-    std::vector<uint8_t> real(b.n, 0);
-    for (int i = 0; i < b.n_eff; ++i) {
-      if (b.vidx[i] == 0xFFFFFFFFu) continue;
-      real[i] = s->h_valid[b.vidx[i]];
-      redo = redo || (b.consulted[i] && !real[i]);
-    }
-    if (!redo) continue;
-    plan_batch(*s, b, real, fix_out);
-    fix_out = b.plan.out_bytes;
-    const uint32_t seg0 = (uint32_t)fix_segs.size();
-    for (GroItem it : b.plan.items) {
-      it.seg_first += seg0;
-      fix_items.push_back(it);
-    }
-    fix_segs.insert(fix_segs.end(), b.plan.segs.begin(), b.plan.segs.end());
-    b.fixup = true;
-  }
-  if (!fix_items.empty()) {
-    hipSetDevice(ws->ctx->device);
-    const size_t ib = fix_items.size() * sizeof(GroItem), sb = fix_segs.size() * sizeof(GroSeg);
-    if (ib + sb > ws->max_meta) return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: re-plan too large");
-    if (fix_out + 16 > s->fix_cap) {
-      if (s->h_fix) hipHostFree(s->h_fix);
-      if (s->d_fix) hipFree(s->d_fix);
-      s->h_fix = nullptr;
-      s->d_fix = nullptr;
-      s->fix_cap = 0;
-      const size_t want = al16(fix_out + fix_out / 4 + 4096);
-      e = hipHostMalloc((void**)&s->h_fix, want, hipHostMallocDefault);
-      if (e == hipSuccess) e = hipMalloc((void**)&s->d_fix, want);
-      if (e != hipSuccess) return hip_fail(ws->ctx, e, "wstager: fixup region");
-      s->fix_cap = want;
-    }
-    memcpy(s->h_meta, fix_items.data(), ib);
-    memcpy(s->h_meta + ib, fix_segs.data(), sb);
-    e = hipMemcpyAsync(s->d_meta, s->h_meta, ib + sb, hipMemcpyHostToDevice, s->stream);
-    if (e == hipSuccess)
-      e = launch_gro_coalesce(s->d_stage, (const GroItem*)s->d_meta, (uint32_t)fix_items.size(),
-                              (const GroSeg*)(s->d_meta + ib), (uint32_t)fix_segs.size(), s->d_fix, s->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(s->h_fix, s->d_fix, fix_out, hipMemcpyDeviceToHost, s->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
-    if (e != hipSuccess) return hip_fail(ws->ctx, e, "wstager re-plan");
-  }
-  // the zero virtio header of NOOP buffers (gro.go:1350-1356) and of unmerged
-  // items (applyTCPCoalesce / applyUDPCoalesce, gro.go:1168-1174), into the
-  // staged headroom of the buffer now at that slot (H2D is long done)
-  for (const WBatch& b : s->batches) {
-    if (b.status) continue;
-    for (int slot : b.plan.zero_hdr) memset(s->h_stage + b.stage[b.order[slot]] - kVnetLen, 0, kVnetLen);
-  }
   s->state = 3;
   return WGCS_OK;
 }
 
-// What Tun.Write(bufs, offset) of batch `write_idx` hands to write(2)
+// What Tun.Write(bufs, offset) of call `write_idx` hands to write(2)
 // (tun.go:679-698): status (0 or INVALID_OFFSET -- then nothing is written),
 // to_write[k] (handleGRO's toWrite), and for each k the bytes
 // bufs[to_write[k]][offset-10:len] after handleGRO: pkts[k] (pinned, valid
@@ -435,27 +354,26 @@ int wgcs_wstager_result(wgcs_wstager* ws, uint64_t batch, int write_idx, int* st
   if (!ws || !status || !n_write) return WGCS_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(ws->mu);
   WSlot* s = ws->find(batch);
-  if (!s || s->state != 3) return WGCS_ERR_NOT_READY;
-  if (write_idx < 0 || (size_t)write_idx >= s->batches.size()) return WGCS_ERR_INVALID_ARG;
-  const WBatch& b = s->batches[write_idx];
-  *status = b.status;
+  if (!s || s->state == 1 || (s->state == 2 && hipEventQuery(s->done) != hipSuccess)) return WGCS_ERR_NOT_READY;
+  if (write_idx < 0 || (size_t)write_idx >= s->calls.size()) return WGCS_ERR_INVALID_ARG;
+  const WCall& c = s->calls[write_idx];
   *n_write = 0;
-  if (b.status) return WGCS_OK;  // Tun.Write returns (0, err) before writing (tun.go:674-676)
-  if ((int)b.plan.to_write.size() > 0 && (!to_write || !pkts || !pkt_lens)) return WGCS_ERR_INVALID_ARG;
-  const uint8_t* out = b.fixup ? s->h_fix : s->h_out;
-  int k = 0;
-  for (int i : b.plan.to_write) {
-    to_write[k] = i;
-    const size_t ln = b.lens[i] - (size_t)b.offset + kVnetLen;
-    const uint8_t* p = nullptr;
-    for (size_t t = 0; t < b.plan.items.size(); ++t)
-      if (b.plan.item_slot[t] == i) p = out + b.plan.items[t].out_off;  // merged super-packet (apply*)
-    if (!p) p = s->h_stage + b.stage[b.order[i]] - kVnetLen;         // zero virtio header + the packet as pushed
-    pkts[k] = p;
-    pkt_lens[k] = ln;
-    ++k;
+  *status = c.status;
+  if (c.dev < 0) return WGCS_OK;  // Tun.Write returns (0, err) before writing (tun.go:674-676), or n == 0
+  *status = s->res_status()[c.dev];
+  if (*status) return WGCS_OK;
+  const int nw = s->res_nwrite()[c.dev];
+  if (nw > 0 && (!to_write || !pkts || !pkt_lens)) return WGCS_ERR_INVALID_ARG;
+  const int32_t* tw = s->res_towrite() + c.first;
+  const int32_t* wl = s->res_wlen() + c.first;
+  uint64_t pos = c.base;
+  for (int k = 0; k < nw; ++k) {
+    to_write[k] = tw[k];
+    pkts[k] = s->h_out + pos + (kHead - kVnet);
+    pkt_lens[k] = (size_t)wl[k];
+    pos += kHead + al16((size_t)wl[k] - kVnet);
   }
-  *n_write = k;
+  *n_write = nw;
   return WGCS_OK;
 }
 

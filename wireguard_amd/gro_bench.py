@@ -127,8 +127,9 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
 def run_staged(args, torch, dev, dist, rank, world, local, barrier, calls_per_slot: int = 64, depth: int = 3):
     """bench.py --config gro_staged: the Tun.Write stager (wgcs_wstager_*).
     One step = one ring slot of `calls_per_slot` Write calls (128 packets
-    each, the batch above): push (pinned staging + host flow plan), submit
-    (H2D, one VALIDATE + one coalesce launch, D2H), and -- depth-1 slots later
+    each, the batch above): push (pinned staging, no host planning), submit
+    (H2D, scatter into Go-sized slices, ONE device handleGRO launch over every
+    call, gather of the write(2) images, D2H), and -- depth-1 slots later
     -- wait + per-call results (the write(2) images).  Host buffers in, host
     buffers out: PCIe-inclusive packets/s."""
     import ctypes as C

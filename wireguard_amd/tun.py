@@ -320,8 +320,8 @@ class Stager:
 
 class WriteStager:
     """Tun.Write batch staging ring (include/wgcsum.h wgcs_wstager_*): many
-    Write calls -> one VALIDATE + one coalesce launch, pipelined H2D / kernels /
-    D2H.  push(bufs, lens, offset) stages one Write call (bufs: numpy arrays of
+    Write calls -> one device-resident handleGRO launch (one workgroup per
+    call), pipelined H2D / kernels / D2H.  push(bufs, lens, offset) stages one Write call (bufs: numpy arrays of
     cap(bufs[i]) bytes holding len lens[i], the packet at [offset:lens[i]]);
     result() returns what Tun.Write would write(2) for it (tun/tun.go:687-698)."""
 
