@@ -170,3 +170,36 @@ def test_write_stager_rejects_oversized_call(dev):
         ws.push(bufs, lens, OFFSET, True)
     assert getattr(ei.value, "code", None) == -1, ei.value
     ws.close()
+
+
+def test_write_stager_concurrent_pushes(dev):
+    """Write calls pushed from 4 threads at once (the packet copies run outside
+    the stager's lock): every call's results still match its own handleGRO."""
+    import threading
+
+    calls = _calls(5)[:16]
+    ws = WriteStager(dev, depth=2, max_writes=16, max_pkts=16 * 128, max_bytes=16 * 128 * 1600)
+    staged = [None] * len(calls)
+    keep = []
+
+    def worker(t):
+        for k in range(t, len(calls), 4):
+            pkts, cap, can_udp, lo = calls[k]
+            bufs, lens = _mk(pkts, cap, OFFSET, lo)
+            keep.append(bufs)
+            staged[k] = ws.push(bufs, lens, OFFSET, can_udp)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert sorted(staged) == list(range(len(calls)))
+    b = ws.submit()
+    ws.wait(b)
+    for k, (pkts, cap, can_udp, lo) in enumerate(calls):
+        rc, tw, writes = _oracle_writes(pkts, cap, can_udp, OFFSET, lo)
+        err, tw_p, writes_p = ws.result(b, staged[k], len(pkts))
+        assert (0 if err is None else err.code, tw_p) == (rc, tw), k
+        assert writes_p == writes, f"call {k}: {_first_diff(writes_p, writes)}"
+    ws.close()

@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -67,6 +68,7 @@ struct WSlot {
   size_t used = 0;      // staged bytes (and output bytes)
   uint64_t arena = 0;   // device arena bytes of the staged slices
   uint32_t npk = 0, ndev = 0;
+  int copying = 0;      // pushes whose packet copies into h_stage are still running
   // pinned host
   uint8_t* h_stage = nullptr;
   wgcs_gro_buf* h_bufs = nullptr;
@@ -104,6 +106,7 @@ struct wgcs_wstager {
   uint32_t open = 0;
   uint64_t next_id = 1;
   std::mutex mu;
+  std::condition_variable copied;  // a push finished copying into its slot
   WSlot* find(uint64_t id) {
     for (auto& s : slots)
       if (s.id == id && id != 0) return &s;
@@ -137,6 +140,7 @@ int open_wslot(wgcs_wstager* ws, uint32_t idx) {
   s.used = 0;
   s.arena = 0;
   s.npk = s.ndev = 0;
+  s.copying = 0;
   ws->open = idx;
   return WGCS_OK;
 }
@@ -209,15 +213,16 @@ int wgcs_wstager_destroy(wgcs_wstager* ws) {
 
 // Stage one Tun.Write(bufs, offset) call: bufs[i] is a Go slice, its packet at
 // bufs[i][offset:lens[i]], cap(bufs[i]) = caps[i] (device/receive.go:483).
+// Room and descriptors are reserved under the stager's lock; the packet bytes
+// are copied after it is released, so pushes from many threads (one per
+// peer's RoutineSendToInternet) copy concurrently.  submit waits for the open
+// slot's copies to finish.
 int wgcs_wstager_push(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, const size_t* caps, int n,
                       int offset, int can_udp_gro, int* write_idx) {
   if (!ws || !write_idx || n < 0 || (n > 0 && (!bufs || !lens || !caps))) return WGCS_ERR_INVALID_ARG;
   if (n > WGCS_GRO_MAX_CALL)
     return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: %d buffers in one Write call (at most %d)", n,
                    WGCS_GRO_MAX_CALL);
-  std::lock_guard<std::mutex> g(ws->mu);
-  WSlot& s = ws->slots[ws->open];
-  if (s.calls.size() >= ws->max_writes) return set_err(ws->ctx, WGCS_ERR_BATCH_FULL, "wstager: open batch is full");
   WCall c;
   c.n = n;
   c.offset = offset;
@@ -229,64 +234,86 @@ int wgcs_wstager_push(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t
       c.status = WGCS_ERR_INVALID_OFFSET;
       break;
     }
-  if (c.status || n == 0) {
-    *write_idx = (int)s.calls.size();
-    s.calls.push_back(c);
-    return WGCS_OK;
-  }
   size_t need = 0;
   uint64_t arena = 0;
-  for (int i = 0; i < n; ++i) {
-    if (caps[i] < lens[i] || caps[i] > 0xFFFFFFFFull)
-      return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: cap(bufs[%d]) < len or >= 4 GiB", i);
-    need += kHead + al16(lens[i] - offset);
-    arena += 32 + al16((size_t)offset) + al16(caps[i] - offset);
+  if (!c.status)
+    for (int i = 0; i < n; ++i) {
+      if (caps[i] < lens[i] || caps[i] > 0xFFFFFFFFull)
+        return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: cap(bufs[%d]) < len or >= 4 GiB", i);
+      need += kHead + al16(lens[i] - offset);
+      arena += 32 + al16((size_t)offset) + al16(caps[i] - offset);
+    }
+  uint8_t* stage;
+  uint64_t at;
+  WSlot* sp;
+  {
+    std::lock_guard<std::mutex> g(ws->mu);
+    WSlot& s = ws->slots[ws->open];
+    if (s.calls.size() >= ws->max_writes) return set_err(ws->ctx, WGCS_ERR_BATCH_FULL, "wstager: open batch is full");
+    if (c.status || n == 0) {
+      *write_idx = (int)s.calls.size();
+      s.calls.push_back(c);
+      return WGCS_OK;
+    }
+    if (s.npk + (uint32_t)n > ws->max_pkts || s.used + need > ws->max_bytes)
+      return set_err(ws->ctx, WGCS_ERR_BATCH_FULL, "wstager: open batch is full");
+    c.dev = (int)s.ndev;
+    c.first = s.npk;
+    c.base = s.used;
+    at = s.used;
+    for (int i = 0; i < n; ++i) {
+      const size_t pl = lens[i] - (size_t)offset;
+      const uint64_t pkt = s.arena + 16 + al16((size_t)offset);  // the packet in the arena (16-byte aligned)
+      wgcs_gro_buf& b = s.h_bufs[s.npk];
+      b.off = pkt - (uint64_t)offset;
+      b.len = (uint32_t)lens[i];
+      b.cap = (uint32_t)caps[i];
+      WsMove& m = s.h_moves[s.npk];
+      m.src = s.used;  // headroom chunk, then the packet (16-byte aligned)
+      m.dst = pkt - kHead;
+      m.n16 = (uint32_t)((kHead + al16(pl)) >> 4);
+      m.pad = 0;
+      s.used += kHead + al16(pl);
+      s.arena += 32 + al16((size_t)offset) + al16(caps[i] - offset);
+      ++s.npk;
+    }
+    wgcs_gro_call& dc = s.h_calls[s.ndev];
+    dc.first = c.first;
+    dc.n = (uint32_t)n;
+    dc.offset = offset;
+    dc.flags = can_udp_gro ? WGCS_GRO_CAN_UDP : 0u;
+    WsOut& o = s.h_outs[s.ndev];
+    o.base = c.base;
+    o.room = (uint32_t)need;
+    o.pad = 0;
+    ++s.ndev;
+    *write_idx = (int)s.calls.size();
+    s.calls.push_back(c);
+    ++s.copying;
+    stage = s.h_stage;
+    sp = &s;
   }
-  if (s.npk + (uint32_t)n > ws->max_pkts || s.used + need > ws->max_bytes)
-    return set_err(ws->ctx, WGCS_ERR_BATCH_FULL, "wstager: open batch is full");
-  c.dev = (int)s.ndev;
-  c.first = s.npk;
-  c.base = s.used;
-  for (int i = 0; i < n; ++i) {
+  for (int i = 0; i < n; ++i) {  // headroom: 6 zero bytes + bufs[i][offset-10:offset], then the packet
     const size_t pl = lens[i] - (size_t)offset;
-    const uint64_t at = s.used + kHead;  // the packet in the stage (16-byte aligned)
-    memset(s.h_stage + s.used, 0, kHead - kVnet);
-    memcpy(s.h_stage + at - kVnet, bufs[i] + offset - kVnet, kVnet);
-    memcpy(s.h_stage + at, bufs[i] + offset, pl);
-    s.used = at + al16(pl);
-    const uint64_t pkt = s.arena + 16 + al16((size_t)offset);  // the packet in the arena (16-byte aligned)
-    wgcs_gro_buf& b = s.h_bufs[s.npk];
-    b.off = pkt - (uint64_t)offset;
-    b.len = (uint32_t)lens[i];
-    b.cap = (uint32_t)caps[i];
-    WsMove& m = s.h_moves[s.npk];
-    m.src = at - kHead;
-    m.dst = pkt - kHead;
-    m.n16 = (uint32_t)((kHead + al16(pl)) >> 4);
-    m.pad = 0;
-    s.arena += 32 + al16((size_t)offset) + al16(caps[i] - offset);
-    ++s.npk;
+    memset(stage + at, 0, kHead - kVnet);
+    memcpy(stage + at + kHead - kVnet, bufs[i] + offset - kVnet, kVnet);
+    memcpy(stage + at + kHead, bufs[i] + offset, pl);
+    at += kHead + al16(pl);
   }
-  wgcs_gro_call& dc = s.h_calls[s.ndev];
-  dc.first = c.first;
-  dc.n = (uint32_t)n;
-  dc.offset = offset;
-  dc.flags = can_udp_gro ? WGCS_GRO_CAN_UDP : 0u;
-  WsOut& o = s.h_outs[s.ndev];
-  o.base = c.base;
-  o.room = (uint32_t)(s.used - c.base);
-  o.pad = 0;
-  ++s.ndev;
-  *write_idx = (int)s.calls.size();
-  s.calls.push_back(c);
+  {
+    std::lock_guard<std::mutex> g(ws->mu);
+    --sp->copying;
+  }
+  ws->copied.notify_all();
   return WGCS_OK;
 }
 
 int wgcs_wstager_submit(wgcs_wstager* ws, uint64_t* batch) {
   if (!ws || !batch) return WGCS_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> g(ws->mu);
+  std::unique_lock<std::mutex> g(ws->mu);
   hipSetDevice(ws->ctx->device);
   WSlot& s = ws->slots[ws->open];
+  ws->copied.wait(g, [&] { return s.copying == 0; });  // pushes still copying into this slot
   const hipStream_t q = s.stream;
   hipError_t e = hipSuccess;
   if (s.ndev) {

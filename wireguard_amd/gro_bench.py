@@ -133,9 +133,12 @@ def run_staged(args, torch, dev, dist, rank, world, local, barrier, calls_per_sl
     -- wait + per-call results (the write(2) images).  Host buffers in, host
     buffers out: PCIe-inclusive packets/s."""
     import ctypes as C
+    import os
 
     from .tun import WriteStager
 
+    calls_per_slot = int(os.environ.get("WGCS_WS_CALLS", calls_per_slot))
+    depth = int(os.environ.get("WGCS_WS_DEPTH", depth))
     pkts = make_batch(dev)
     n = len(pkts)
     b = Batch(pkts)
@@ -148,7 +151,6 @@ def run_staged(args, torch, dev, dist, rank, world, local, barrier, calls_per_sl
     tw = (C.c_int * n)()
     outp = (C.c_void_p * n)()
     outl = (C.c_size_t * n)()
-    idx = C.c_int(0)
     bt = C.c_uint64(0)
     inflight = []
 
@@ -158,17 +160,44 @@ def run_staged(args, torch, dev, dist, rank, world, local, barrier, calls_per_sl
             L.wgcs_wstager_result(ws.h, batch, k, C.byref(st), C.byref(nw), tw, outp, outl)
             assert st.value == 0 and nw.value == 4, (st.value, nw.value)
 
+    # Write calls arrive from many goroutines (one RoutineSendToInternet per
+    # peer): `threads` host threads push concurrently (ctypes releases the GIL;
+    # the stager copies outside its lock)
+    import concurrent.futures as cf
+
+    threads = max(1, int(getattr(args, "push_threads", 0) or os.environ.get("WGCS_PUSH_THREADS", 1)))
+    pool = cf.ThreadPoolExecutor(threads) if threads > 1 else None
+    share = [calls_per_slot // threads + (1 if t < calls_per_slot % threads else 0) for t in range(threads)]
+
+    def pusher(k):
+        i = C.c_int(0)
+        for _ in range(k):
+            assert L.wgcs_wstager_push(ws.h, ptrs, b.lens0, b.caps, n, OFFSET, 1, C.byref(i)) == 0
+
+    phase = [0.0, 0.0, 0.0]  # push, wait + results, submit (host seconds)
+
     def step():
-        for _ in range(calls_per_slot):
-            assert L.wgcs_wstager_push(ws.h, ptrs, b.lens0, b.caps, n, OFFSET, 1, C.byref(idx)) == 0
+        t0 = time.perf_counter()
+        if pool is None:
+            pusher(calls_per_slot)
+        else:
+            for f in [pool.submit(pusher, k) for k in share]:
+                f.result()
+        t1 = time.perf_counter()
         if len(inflight) == depth - 1:
             settle(inflight.pop(0))
+        t2 = time.perf_counter()
         assert L.wgcs_wstager_submit(ws.h, C.byref(bt)) == 0
         inflight.append(bt.value)
+        t3 = time.perf_counter()
+        phase[0] += t1 - t0
+        phase[1] += t2 - t1
+        phase[2] += t3 - t2
 
     for _ in range(max(args.warmup, depth + 1)):
         step()
     barrier()
+    phase[:] = [0.0, 0.0, 0.0]
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -178,6 +207,8 @@ def run_staged(args, torch, dev, dist, rank, world, local, barrier, calls_per_sl
     dt = shard.max_over_ranks(time.perf_counter() - t0, dist)
     per = dt / args.steps
     ws.close()
+    if pool is not None:
+        pool.shutdown()
     # the written images are correct: one slot checked against the oracle in tests/test_gpu_wstager.py
     result = {
         "metric": "Tun.Write handleGRO packets/s through the write stager (host buffers in, write(2) images out)",
@@ -197,6 +228,10 @@ def run_staged(args, torch, dev, dist, rank, world, local, barrier, calls_per_sl
                         f"ring slot, depth {depth}; each call coalesced to 4 super-packets",
             "packets_per_step": calls_per_slot * n,
             "payload_bytes_per_step": calls_per_slot * sum(len(p) for p in pkts),
+            "push_threads": threads,
+            "host_ms_per_step": {"push": round(phase[0] / args.steps * 1e3, 4),
+                                 "wait_and_results": round(phase[1] / args.steps * 1e3, 4),
+                                 "submit": round(phase[2] / args.steps * 1e3, 4)},
             "parallelism": f"replica{world} (one stager per GPU, no collective)",
             "gib_per_s": round(calls_per_slot * sum(len(p) for p in pkts) / per / 2**30, 3),
         },
