@@ -288,7 +288,9 @@ def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int =
     for i, p in enumerate(pkts):
         img[i, OFFSET: OFFSET + len(p)] = np.frombuffer(p, np.uint8)
     d_img = torch.from_numpy(np.tile(img, (calls, 1))).cuda()
-    R = max(1, rotate)
+    # rotated copies (each launch's packets alone exceed the 256 MiB MALL), at
+    # most ~64 GiB of slices in all, at least 2 (consecutive launches overlap)
+    R = max(2, min(rotate, (64 << 30) // (N * stride)))
     arenas = [torch.empty(N * stride, dtype=torch.uint8, device="cuda") for _ in range(R)]
     gb = np.zeros(N, GRO_BUF_DTYPE)
     gb["off"] = np.arange(N, dtype=np.uint64) * np.uint64(stride)
