@@ -143,6 +143,10 @@ const char *wgcs_last_error(wgcs_ctx *ctx);
 int wgcs_sync(wgcs_ctx *ctx);
 /* CU count of the context's device (grid sizing, reporting) */
 int wgcs_num_cu(wgcs_ctx *ctx);
+/* Pinned host memory mapped into the device's address space at the same
+ * address (bytes rounded up to 16): the buffers of wgcs_wstager_push_pinned. */
+int wgcs_host_alloc(wgcs_ctx *ctx, size_t bytes, void **p);
+int wgcs_host_free(wgcs_ctx *ctx, void *p);
 
 /* ---- device-resident batch entry points (HBM in, HBM out; async on stream) ----
  * The arena must be readable through align_up(off+len, 16) for every packet
@@ -289,6 +293,13 @@ int wgcs_wstager_destroy(wgcs_wstager *ws);
  * (WGCS_ERR_BATCH_FULL: submit first) */
 int wgcs_wstager_push(wgcs_wstager *ws, const uint8_t *const *bufs, const size_t *lens, const size_t *caps, int n,
                       int offset, int can_udp_gro, int *write_idx);
+/* Zero-copy form: every bufs[i] lies in memory from wgcs_host_alloc and stays
+ * unchanged until the slot's results have been read; push records descriptors
+ * only and the slot's scatter kernel reads the packets from host memory over
+ * PCIe (a buffer pool allocated this way, e.g. device.pools.messageBufs, lets
+ * Write skip the staging copy). */
+int wgcs_wstager_push_pinned(wgcs_wstager *ws, const uint8_t *const *bufs, const size_t *lens, const size_t *caps,
+                             int n, int offset, int can_udp_gro, int *write_idx);
 int wgcs_wstager_submit(wgcs_wstager *ws, uint64_t *batch);
 int wgcs_wstager_wait(wgcs_wstager *ws, uint64_t batch);
 /* to_write / pkts / pkt_lens hold at least n (the call's packet count) entries */

@@ -203,3 +203,59 @@ def test_write_stager_concurrent_pushes(dev):
         assert (0 if err is None else err.code, tw_p) == (rc, tw), k
         assert writes_p == writes, f"call {k}: {_first_diff(writes_p, writes)}"
     ws.close()
+
+
+def _mk_pinned(pool, at, pkts, cap, offset, lens_override, phase):
+    """The packets in Go-slice buffers carved out of pinned host memory
+    (Device.host_alloc) at 16-byte phases `phase(i)`; returns (bufs, lens, at)."""
+    bufs, lens = [], []
+    for i, p in enumerate(pkts):
+        c = cap if isinstance(cap, int) else cap(len(p))
+        at += phase(i)
+        b = pool[at: at + c]
+        b[:] = 0x5A
+        b[offset: offset + len(p)] = np.frombuffer(p, np.uint8)
+        bufs.append(b)
+        lens.append(offset + len(p))
+        at = (at + c + 15) // 16 * 16
+    for i, ln in (lens_override or {}).items():
+        lens[i] = ln
+    return bufs, lens, at
+
+
+def test_write_stager_pinned_zero_copy(dev):
+    """wgcs_wstager_push_pinned: the scatter kernel reads the packets straight
+    from pinned host memory (buffers at every 16-byte phase), mixed in one slot
+    with copying pushes; every call's write(2) images equal handleGRO's."""
+    calls = _calls(6)[:12]
+    total = sum(sum((c if isinstance(c, int) else c(len(p))) + 32 for p in pk) for pk, c, _, _ in calls)
+    pool = dev.host_alloc(total + 4096)
+    ws = WriteStager(dev, depth=2, max_writes=16, max_pkts=16 * 128, max_bytes=16 * 128 * 1600)
+    at, idxs, keep = 0, [], []
+    for k, (pkts, cap, can_udp, lo) in enumerate(calls):
+        if k % 3 == 2:  # a copying push in between
+            bufs, lens = _mk(pkts, cap, OFFSET, lo)
+            keep.append(bufs)
+            idxs.append(ws.push(bufs, lens, OFFSET, can_udp))
+        else:
+            bufs, lens, at = _mk_pinned(pool, at, pkts, cap, OFFSET, lo, lambda i, k=k: (i * 7 + k) % 16)
+            idxs.append(ws.push_pinned(bufs, lens, OFFSET, can_udp))
+    b = ws.submit()
+    ws.wait(b)
+    for k, (pkts, cap, can_udp, lo) in enumerate(calls):
+        rc, tw, writes = _oracle_writes(pkts, cap, can_udp, OFFSET, lo)
+        err, tw_p, writes_p = ws.result(b, idxs[k], len(pkts))
+        assert (0 if err is None else err.code, tw_p) == (rc, tw), k
+        assert writes_p == writes, f"call {k}: {_first_diff(writes_p, writes)}"
+    ws.close()
+    dev.host_free(pool)
+
+
+def test_write_stager_pinned_rejects_pageable(dev):
+    """push_pinned refuses buffers that are not wgcs_host_alloc memory."""
+    ws = WriteStager(dev, depth=2, max_writes=4, max_pkts=512, max_bytes=512 * 1600)
+    bufs, lens = _mk(flow(4, seed=9))
+    with pytest.raises(Exception) as ei:
+        ws.push_pinned(bufs, lens, OFFSET, True)
+    assert getattr(ei.value, "code", None) == -1, ei.value
+    ws.close()

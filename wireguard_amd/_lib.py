@@ -122,7 +122,11 @@ def load() -> C.CDLL:
         "wgcs_wstager_create": ([vp, u32, u32, u32, sz, C.POINTER(vp)], i32),
         "wgcs_wstager_destroy": ([vp], i32),
         "wgcs_wstager_push": ([vp, C.POINTER(vp), C.POINTER(sz), C.POINTER(sz), i32, i32, i32, C.POINTER(i32)], i32),
+        "wgcs_wstager_push_pinned": ([vp, C.POINTER(vp), C.POINTER(sz), C.POINTER(sz), i32, i32, i32,
+                                      C.POINTER(i32)], i32),
         "wgcs_wstager_submit": ([vp, C.POINTER(u64)], i32),
+        "wgcs_host_alloc": ([vp, sz, C.POINTER(vp)], i32),
+        "wgcs_host_free": ([vp, vp], i32),
         "wgcs_wstager_wait": ([vp, u64], i32),
         "wgcs_wstager_result": ([vp, u64, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(vp),
                                  C.POINTER(sz)], i32),

@@ -4,6 +4,8 @@
 // fallback: if HIP or the device is unavailable every call fails loudly.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -57,6 +59,14 @@ int ensure_pinned(wgcs_ctx* ctx, HostBuf& b, size_t bytes) {
   if (e != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc");
   b.cap = want;
   return WGCS_OK;
+}
+
+bool host_mapped(wgcs_ctx* ctx, const void* p, size_t n) {
+  const uintptr_t a = (uintptr_t)p, b = a + n;
+  std::lock_guard<std::mutex> g(ctx->host_mu);
+  for (const auto& r : ctx->host_allocs)
+    if (a >= r.first && b <= r.second && b >= a) return true;
+  return false;
 }
 
 }  // namespace wgcs
@@ -114,10 +124,51 @@ int wgcs_init(int device, wgcs_ctx** out) {
   return WGCS_OK;
 }
 
+// Pinned host memory the device reads directly (zero-copy Write staging,
+// wgcs_wstager_push_pinned).  HIP maps hipHostMalloc memory into the device's
+// address space at the same address; that is checked once here, so kernels
+// can take the host pointers as they are.
+int wgcs_host_alloc(wgcs_ctx* ctx, size_t bytes, void** p) {
+  if (!ctx || !p || bytes == 0) return WGCS_ERR_INVALID_ARG;
+  *p = nullptr;
+  hipSetDevice(ctx->device);
+  const size_t n = (bytes + 15) & ~(size_t)15;
+  void* h = nullptr;
+  hipError_t e = hipHostMalloc(&h, n, hipHostMallocDefault);
+  if (e != hipSuccess) return hip_fail(ctx, e, "wgcs_host_alloc");
+  void* d = nullptr;
+  e = hipHostGetDevicePointer(&d, h, 0);
+  if (e != hipSuccess || d != h) {
+    hipHostFree(h);
+    return e != hipSuccess ? hip_fail(ctx, e, "hipHostGetDevicePointer")
+                           : set_err(ctx, WGCS_ERR_HIP, "pinned memory is not mapped at its host address");
+  }
+  std::lock_guard<std::mutex> g(ctx->host_mu);
+  ctx->host_allocs.emplace_back((uintptr_t)h, (uintptr_t)h + n);
+  *p = h;
+  return WGCS_OK;
+}
+
+int wgcs_host_free(wgcs_ctx* ctx, void* p) {
+  if (!ctx || !p) return WGCS_ERR_INVALID_ARG;
+  {
+    std::lock_guard<std::mutex> g(ctx->host_mu);
+    auto& v = ctx->host_allocs;
+    auto it = std::find_if(v.begin(), v.end(), [&](const std::pair<uintptr_t, uintptr_t>& r) {
+      return r.first == (uintptr_t)p;
+    });
+    if (it == v.end()) return set_err(ctx, WGCS_ERR_INVALID_ARG, "wgcs_host_free: not a wgcs_host_alloc pointer");
+    v.erase(it);
+  }
+  const hipError_t e = hipHostFree(p);
+  return e == hipSuccess ? WGCS_OK : hip_fail(ctx, e, "hipHostFree");
+}
+
 int wgcs_destroy(wgcs_ctx* ctx) {
   if (!ctx) return WGCS_ERR_INVALID_ARG;
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  for (const auto& r : ctx->host_allocs) hipHostFree((void*)r.first);
   for (DevBuf* b : {&ctx->d_arena, &ctx->d_pkts, &ctx->d_init, &ctx->d_out, &ctx->d_out2, &ctx->d_aux})
     if (b->ptr) hipFree(b->ptr);
   for (HostBuf* b : {&ctx->h_stage, &ctx->h_meta, &ctx->h_out})

@@ -675,8 +675,10 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
 
 // ---- write stager (wstager.cpp): staged packets -> slices, toWrite images -> packed output
 //
-// One wave per staged packet: its 16 bytes of headroom (virtio header) and
-// packet, aligned 16-byte chunks from the packed stage into its slice.
+// One wave per staged packet: the aligned 16-byte chunks that hold its
+// virtio header and packet, from the packed stage (or, for zero-copy pushes,
+// straight from pinned host memory over PCIe) into its slice, which has the
+// same phase mod 16.
 __global__ __launch_bounds__(256) void ws_scatter_kernel(const uint8_t* __restrict__ stage,
                                                          uint8_t* __restrict__ arena, const WsMove* __restrict__ mv,
                                                          uint32_t n) {
@@ -684,7 +686,8 @@ __global__ __launch_bounds__(256) void ws_scatter_kernel(const uint8_t* __restri
   const uint32_t lane = threadIdx.x & 63u;
   if (w >= n) return;  // wave-uniform
   const WsMove m = mv[w];
-  const uint4* s = reinterpret_cast<const uint4*>(stage + m.src);
+  const uint4* s = (m.flags & WS_MOVE_ABS) ? reinterpret_cast<const uint4*>((uintptr_t)m.src)
+                                           : reinterpret_cast<const uint4*>(stage + m.src);
   uint4* d = reinterpret_cast<uint4*>(arena + m.dst);
   uint32_t k = lane;
   for (; k + 64 < m.n16; k += 128) {  // two chunks per lane in flight
@@ -697,19 +700,22 @@ __global__ __launch_bounds__(256) void ws_scatter_kernel(const uint8_t* __restri
 
 // One block per call: Tun.Write's write(2) images, bufs[i][offset-10:len] for
 // i in toWrite (tun.go:687-698), packed in toWrite order into the call's
-// output region; entry k takes 16 + align16(len - offset) bytes starting with
-// the aligned chunk that holds the virtio header, so its image starts 6 bytes
-// in.  wlen[first + k] = its length.  An image set larger than the region
-// (not possible: each packet's bytes end up in at most one written buffer)
-// would be reported as WGCS_ERR_OUT_OF_RANGE, never written past it.
+// output region as the aligned 16-byte chunks that hold them (so source and
+// destination share their phase mod 16); wlen / wpos[first + k] = the image's
+// length and its first byte in the region.  An image set larger than the
+// region (not possible: each packet's bytes end up in at most one written
+// buffer, and the host reserves 32 + align16(len) bytes per packet) would be
+// reported as WGCS_ERR_OUT_OF_RANGE, never written past it.
 __global__ __launch_bounds__(256) void ws_gather_kernel(const uint8_t* __restrict__ arena,
                                                         const wgcs_gro_buf* __restrict__ bufs,
                                                         const wgcs_gro_call* __restrict__ calls,
                                                         const WsOut* __restrict__ outs, int32_t* __restrict__ status,
                                                         const int32_t* __restrict__ n_write,
                                                         const int32_t* __restrict__ to_write,
-                                                        int32_t* __restrict__ wlen, uint8_t* __restrict__ out) {
+                                                        int32_t* __restrict__ wlen, int32_t* __restrict__ wpos,
+                                                        uint8_t* __restrict__ out) {
   __shared__ uint32_t pos[kMaxB + 1];
+  __shared__ uint32_t lead[kMaxB];
   __shared__ uint64_t src[kMaxB];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const wgcs_gro_call call = calls[blockIdx.x];
@@ -720,10 +726,12 @@ __global__ __launch_bounds__(256) void ws_gather_kernel(const uint8_t* __restric
   if (t < nw) {
     const int i = to_write[call.first + t];
     const wgcs_gro_buf b = bufs[call.first + i];
-    const uint32_t pl = b.len - (uint32_t)call.offset;
-    wlen[call.first + t] = (int32_t)(pl + kVnet);
-    pos[t + 1] = 16u + ((pl + 15u) & ~15u);
-    src[t] = b.off + (uint64_t)call.offset - 16u;
+    const uint64_t img = b.off + (uint64_t)call.offset - kVnet;  // bufs[i][offset-10]
+    const uint64_t c0 = img & ~(uint64_t)15, c1 = (b.off + b.len + 15) & ~(uint64_t)15;
+    wlen[call.first + t] = (int32_t)(b.len - (uint32_t)call.offset + kVnet);
+    lead[t] = (uint32_t)(img - c0);
+    pos[t + 1] = (uint32_t)(c1 - c0);
+    src[t] = c0;
   }
   __syncthreads();
   if (t == 0) {
@@ -733,6 +741,7 @@ __global__ __launch_bounds__(256) void ws_gather_kernel(const uint8_t* __restric
   }
   __syncthreads();
   if (pos[nw] > o.room) return;  // block-uniform
+  if (t < nw) wpos[call.first + t] = (int32_t)(pos[t] + lead[t]);
   for (int k = wv; k < nw; k += 4) {  // wave-uniform: one image per wave
     const uint4* s = reinterpret_cast<const uint4*>(arena + src[k]);
     uint4* d = reinterpret_cast<uint4*>(out + o.base + pos[k]);
@@ -755,10 +764,10 @@ hipError_t launch_ws_scatter(const uint8_t* stage, uint8_t* arena, const WsMove*
 
 hipError_t launch_ws_gather(const uint8_t* arena, const wgcs_gro_buf* bufs, const wgcs_gro_call* calls,
                             const WsOut* outs, uint32_t n_calls, int32_t* status, const int32_t* n_write,
-                            const int32_t* to_write, int32_t* wlen, uint8_t* out, hipStream_t s) {
+                            const int32_t* to_write, int32_t* wlen, int32_t* wpos, uint8_t* out, hipStream_t s) {
   if (n_calls == 0) return hipSuccess;
   hipLaunchKernelGGL(ws_gather_kernel, dim3(n_calls), dim3(256), 0, s, arena, bufs, calls, outs, status, n_write,
-                     to_write, wlen, out);
+                     to_write, wlen, wpos, out);
   return hipGetLastError();
 }
 

@@ -5,6 +5,8 @@
 
 #include <mutex>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "../../include/wgcsum.h"
 #include "wgcs_kernels.h"
@@ -24,6 +26,8 @@ int set_err(wgcs_ctx* ctx, int code, const char* fmt, ...);
 int hip_fail(wgcs_ctx* ctx, hipError_t e, const char* what);
 int ensure_dev(wgcs_ctx* ctx, DevBuf& b, size_t bytes);
 int ensure_pinned(wgcs_ctx* ctx, HostBuf& b, size_t bytes);
+// [p, p + n) lies inside one wgcs_host_alloc allocation of ctx
+bool host_mapped(wgcs_ctx* ctx, const void* p, size_t n);
 
 }  // namespace wgcs
 
@@ -38,4 +42,7 @@ struct wgcs_ctx {
   wgcs::DevBuf d_arena, d_pkts, d_init, d_out, d_out2, d_aux;
   // pinned host staging
   wgcs::HostBuf h_stage, h_meta, h_out;
+  // wgcs_host_alloc allocations (device-readable pinned memory): [start, end)
+  std::mutex host_mu;
+  std::vector<std::pair<uintptr_t, uintptr_t>> host_allocs;
 };

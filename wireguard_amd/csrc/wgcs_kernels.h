@@ -112,11 +112,13 @@ hipError_t launch_gro_batch(uint8_t* arena, wgcs_gro_buf* bufs, const wgcs_gro_c
 // Write stager around the batched handleGRO (wstager.cpp): packets staged
 // back to back are moved into their Go-sized slices of the device arena, and
 // after the handleGRO launch the toWrite images of each call are packed into
-// that call's output region.  Both copies are 16-byte aligned on both sides.
+// that call's output region.  Source and destination of both copies share
+// their phase mod 16, so both move whole aligned 16-byte chunks.
 struct WsMove {
-  uint64_t src, dst;  // 16-byte aligned stage / arena offsets
-  uint32_t n16, pad;  // 16-byte chunks
+  uint64_t src, dst;    // 16-byte aligned source (stage offset, or a device-visible address) / arena offset
+  uint32_t n16, flags;  // 16-byte chunks; WS_MOVE_ABS: src is an address (pinned host memory)
 };
+enum : uint32_t { WS_MOVE_ABS = 1 };
 struct WsOut {
   uint64_t base;  // the call's output region (16-byte aligned)
   uint32_t room;  // its size in bytes
@@ -125,7 +127,7 @@ struct WsOut {
 hipError_t launch_ws_scatter(const uint8_t* stage, uint8_t* arena, const WsMove* mv, uint32_t n, hipStream_t s);
 hipError_t launch_ws_gather(const uint8_t* arena, const wgcs_gro_buf* bufs, const wgcs_gro_call* calls,
                             const WsOut* outs, uint32_t n_calls, int32_t* status, const int32_t* n_write,
-                            const int32_t* to_write, int32_t* wlen, uint8_t* out, hipStream_t s);
+                            const int32_t* to_write, int32_t* wlen, int32_t* wpos, uint8_t* out, hipStream_t s);
 
 hipError_t launch_gro_coalesce(const uint8_t* stage, const GroItem* items, uint32_t n_items, const GroSeg* segs,
                                uint32_t n_segs, uint8_t* out, hipStream_t s);

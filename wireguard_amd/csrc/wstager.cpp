@@ -21,16 +21,21 @@
 //             index the bytes bufs[i][offset-10:len(bufs[i])] after handleGRO,
 //             in pinned memory (a 10-byte virtio header + packet)
 //
+// wgcs_wstager_push_pinned is the zero-copy form: the caller's buffers live in
+// pinned memory from wgcs_host_alloc, push only records descriptors, and the
+// scatter kernel reads the packets straight from host memory over PCIe.
+//
 // `depth` slots rotate, each with its own stream: slot k's D2H overlaps slot
 // k+1's kernels and slot k+2's H2D.  The caller's buffers are only read by
 // push; handleGRO's in-place edits of bufs are not replayed into them (Write's
 // callers recycle bufs after the call, device/receive.go:500-505).
 //
-// Device arena layout of one staged buffer (16-byte aligned region): 16 B pad,
-// then the slice `off` chosen so that off + offset (the packet) is 16-byte
-// aligned, then cap - offset bytes of slice, 16 B pad.  The scatter copies the
-// headroom chunk + packet as whole aligned chunks; the gather copies the
-// aligned chunk holding the virtio header + the packet as whole chunks.
+// Device arena layout of one staged buffer (16-byte aligned region R): the
+// packet at P = R + 32 + align16(offset) + phase, where phase is the packet's
+// address mod 16 in its source (0 for the packed stage, the caller's for
+// pinned pushes), so source and slice share their phase; the slice `off` =
+// P - offset holds cap bytes; 16+ bytes of pad on both sides.  The scatter and
+// the gather move whole aligned 16-byte chunks.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,6 +50,7 @@
 #include "wgcs_kernels.h"
 
 using namespace wgcs;
+using wgcs::host_mapped;
 
 namespace {
 
@@ -58,14 +64,21 @@ struct WCall {  // one Tun.Write call
   int status = 0;   // 0 or WGCS_ERR_INVALID_OFFSET (gro.go:1335-1337) before the launch
   int dev = -1;     // index among the slot's device calls (-1: nothing staged)
   uint32_t first = 0;
-  uint64_t base = 0;  // its output region in h_out (= its staged bytes)
+  uint64_t out_base = 0;  // its output region in h_out
 };
+
+// Output bytes reserved per packet: its write(2) image as whole aligned chunks
+// (align16(len + 10) + up to 15 bytes of phase) fits in 32 + align16(len).
+inline size_t out_need(size_t pl) { return 32 + al16(pl); }
+// Device arena bytes of one slice
+inline uint64_t arena_need(size_t offset, size_t cap) { return 64 + al16(offset) + al16(cap - offset); }
 
 struct WSlot {
   uint64_t id = 0;
   int state = 0;  // 0 free, 1 open, 2 submitted, 3 done
   std::vector<WCall> calls;
-  size_t used = 0;      // staged bytes (and output bytes)
+  size_t used = 0;      // staged bytes (copying pushes)
+  size_t out_used = 0;  // output region bytes
   uint64_t arena = 0;   // device arena bytes of the staged slices
   uint32_t npk = 0, ndev = 0;
   int copying = 0;      // pushes whose packet copies into h_stage are still running
@@ -75,7 +88,7 @@ struct WSlot {
   WsMove* h_moves = nullptr;
   wgcs_gro_call* h_calls = nullptr;
   WsOut* h_outs = nullptr;
-  int32_t* h_res = nullptr;  // status[ndev] | n_write[ndev] | to_write[npk] | wlen[npk]
+  int32_t* h_res = nullptr;  // status[ndev] | n_write[ndev] | to_write[npk] | wlen[npk] | wpos[npk]
   uint8_t* h_out = nullptr;
   // device
   uint8_t* d_stage = nullptr;
@@ -94,6 +107,7 @@ struct WSlot {
   const int32_t* res_nwrite() const { return h_res + ndev; }
   const int32_t* res_towrite() const { return h_res + 2 * (size_t)ndev; }
   const int32_t* res_wlen() const { return h_res + 2 * (size_t)ndev + npk; }
+  const int32_t* res_wpos() const { return h_res + 2 * (size_t)ndev + 2 * (size_t)npk; }
 };
 
 }  // namespace
@@ -101,7 +115,7 @@ struct WSlot {
 struct wgcs_wstager {
   wgcs_ctx* ctx = nullptr;
   uint32_t depth = 0, max_writes = 0, max_pkts = 0;
-  size_t max_bytes = 0;
+  size_t max_bytes = 0, max_out = 0;
   std::vector<WSlot> slots;
   uint32_t open = 0;
   uint64_t next_id = 1;
@@ -138,6 +152,7 @@ int open_wslot(wgcs_wstager* ws, uint32_t idx) {
   s.state = 1;
   s.calls.clear();
   s.used = 0;
+  s.out_used = 0;
   s.arena = 0;
   s.npk = s.ndev = 0;
   s.copying = 0;
@@ -162,9 +177,10 @@ int wgcs_wstager_create(wgcs_ctx* ctx, uint32_t depth, uint32_t max_writes, uint
   ws->max_writes = max_writes;
   ws->max_pkts = max_pkts;
   ws->max_bytes = al16(max_bytes + (size_t)max_pkts * (kHead + 16));
+  ws->max_out = al16(max_bytes + (size_t)max_pkts * 48);
   ws->slots.resize(depth);
   hipSetDevice(ctx->device);
-  const size_t nres = (2 * (size_t)max_writes + 2 * (size_t)max_pkts) * sizeof(int32_t);
+  const size_t nres = (2 * (size_t)max_writes + 3 * (size_t)max_pkts) * sizeof(int32_t);
   for (auto& s : ws->slots) {
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_stage, ws->max_bytes + 64, hipHostMallocDefault);
@@ -173,14 +189,14 @@ int wgcs_wstager_create(wgcs_ctx* ctx, uint32_t depth, uint32_t max_writes, uint
     if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_calls, max_writes * sizeof(wgcs_gro_call), hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_outs, max_writes * sizeof(WsOut), hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_res, nres, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_out, ws->max_bytes + 64, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&s.h_out, ws->max_out + 64, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMalloc((void**)&s.d_stage, ws->max_bytes + 64);
     if (e == hipSuccess) e = hipMalloc((void**)&s.d_bufs, max_pkts * sizeof(wgcs_gro_buf));
     if (e == hipSuccess) e = hipMalloc((void**)&s.d_moves, max_pkts * sizeof(WsMove));
     if (e == hipSuccess) e = hipMalloc((void**)&s.d_calls, max_writes * sizeof(wgcs_gro_call));
     if (e == hipSuccess) e = hipMalloc((void**)&s.d_outs, max_writes * sizeof(WsOut));
     if (e == hipSuccess) e = hipMalloc((void**)&s.d_res, nres);
-    if (e == hipSuccess) e = hipMalloc((void**)&s.d_out, ws->max_bytes + 64);
+    if (e == hipSuccess) e = hipMalloc((void**)&s.d_out, ws->max_out + 64);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -211,14 +227,17 @@ int wgcs_wstager_destroy(wgcs_wstager* ws) {
   return WGCS_OK;
 }
 
+namespace {
+
 // Stage one Tun.Write(bufs, offset) call: bufs[i] is a Go slice, its packet at
 // bufs[i][offset:lens[i]], cap(bufs[i]) = caps[i] (device/receive.go:483).
-// Room and descriptors are reserved under the stager's lock; the packet bytes
-// are copied after it is released, so pushes from many threads (one per
-// peer's RoutineSendToInternet) copy concurrently.  submit waits for the open
-// slot's copies to finish.
-int wgcs_wstager_push(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, const size_t* caps, int n,
-                      int offset, int can_udp_gro, int* write_idx) {
+// Room and descriptors are reserved under the stager's lock; a copying push
+// copies the packet bytes after releasing it, so pushes from many threads (one
+// per peer's RoutineSendToInternet) copy concurrently, and submit waits for
+// the open slot's copies.  A pinned push copies nothing: its moves point at
+// the caller's pinned buffers.
+int push_call(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, const size_t* caps, int n, int offset,
+              int can_udp_gro, bool pinned, int* write_idx) {
   if (!ws || !write_idx || n < 0 || (n > 0 && (!bufs || !lens || !caps))) return WGCS_ERR_INVALID_ARG;
   if (n > WGCS_GRO_MAX_CALL)
     return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: %d buffers in one Write call (at most %d)", n,
@@ -234,14 +253,15 @@ int wgcs_wstager_push(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t
       c.status = WGCS_ERR_INVALID_OFFSET;
       break;
     }
-  size_t need = 0;
-  uint64_t arena = 0;
+  size_t need = 0, need_out = 0;
   if (!c.status)
     for (int i = 0; i < n; ++i) {
       if (caps[i] < lens[i] || caps[i] > 0xFFFFFFFFull)
         return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: cap(bufs[%d]) < len or >= 4 GiB", i);
-      need += kHead + al16(lens[i] - offset);
-      arena += 32 + al16((size_t)offset) + al16(caps[i] - offset);
+      if (pinned && !host_mapped(ws->ctx, bufs[i] + offset - kVnet, lens[i] - offset + kVnet))
+        return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: bufs[%d] is not in wgcs_host_alloc memory", i);
+      if (!pinned) need += kHead + al16(lens[i] - offset);
+      need_out += out_need(lens[i] - offset);
     }
   uint8_t* stage;
   uint64_t at;
@@ -255,40 +275,55 @@ int wgcs_wstager_push(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t
       s.calls.push_back(c);
       return WGCS_OK;
     }
-    if (s.npk + (uint32_t)n > ws->max_pkts || s.used + need > ws->max_bytes)
+    if (s.npk + (uint32_t)n > ws->max_pkts || s.used + need > ws->max_bytes || s.out_used + need_out > ws->max_out) {
+      if (s.npk == 0)  // would never fit, even in an empty slot: not a BATCH_FULL the caller can retry
+        return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: one Write call exceeds max_pkts / max_bytes");
       return set_err(ws->ctx, WGCS_ERR_BATCH_FULL, "wstager: open batch is full");
+    }
     c.dev = (int)s.ndev;
     c.first = s.npk;
-    c.base = s.used;
+    c.out_base = s.out_used;
     at = s.used;
     for (int i = 0; i < n; ++i) {
       const size_t pl = lens[i] - (size_t)offset;
-      const uint64_t pkt = s.arena + 16 + al16((size_t)offset);  // the packet in the arena (16-byte aligned)
+      const uintptr_t hp = (uintptr_t)(bufs[i] + offset);  // the packet in host memory
+      const uint64_t phase = pinned ? (uint64_t)(hp & 15u) : 0u;
+      const uint64_t pkt = s.arena + 32 + al16((size_t)offset) + phase;  // the packet in the arena
       wgcs_gro_buf& b = s.h_bufs[s.npk];
       b.off = pkt - (uint64_t)offset;
       b.len = (uint32_t)lens[i];
       b.cap = (uint32_t)caps[i];
       WsMove& m = s.h_moves[s.npk];
-      m.src = s.used;  // headroom chunk, then the packet (16-byte aligned)
-      m.dst = pkt - kHead;
-      m.n16 = (uint32_t)((kHead + al16(pl)) >> 4);
-      m.pad = 0;
-      s.used += kHead + al16(pl);
-      s.arena += 32 + al16((size_t)offset) + al16(caps[i] - offset);
+      if (pinned) {  // the aligned chunks holding bufs[i][offset-10:len], read over PCIe
+        const uintptr_t c0 = (hp - kVnet) & ~(uintptr_t)15, c1 = (hp + pl + 15) & ~(uintptr_t)15;
+        m.src = (uint64_t)c0;
+        m.dst = pkt - (uint64_t)(hp - c0);
+        m.n16 = (uint32_t)((c1 - c0) >> 4);
+        m.flags = WS_MOVE_ABS;
+      } else {  // headroom chunk, then the packet (16-byte aligned in the stage)
+        m.src = s.used;
+        m.dst = pkt - kHead;
+        m.n16 = (uint32_t)((kHead + al16(pl)) >> 4);
+        m.flags = 0;
+        s.used += kHead + al16(pl);
+      }
+      s.arena += arena_need((size_t)offset, caps[i]);
       ++s.npk;
     }
+    s.out_used += need_out;
     wgcs_gro_call& dc = s.h_calls[s.ndev];
     dc.first = c.first;
     dc.n = (uint32_t)n;
     dc.offset = offset;
     dc.flags = can_udp_gro ? WGCS_GRO_CAN_UDP : 0u;
     WsOut& o = s.h_outs[s.ndev];
-    o.base = c.base;
-    o.room = (uint32_t)need;
+    o.base = c.out_base;
+    o.room = (uint32_t)need_out;
     o.pad = 0;
     ++s.ndev;
     *write_idx = (int)s.calls.size();
     s.calls.push_back(c);
+    if (pinned) return WGCS_OK;
     ++s.copying;
     stage = s.h_stage;
     sp = &s;
@@ -306,6 +341,18 @@ int wgcs_wstager_push(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t
   }
   ws->copied.notify_all();
   return WGCS_OK;
+}
+
+}  // namespace
+
+int wgcs_wstager_push(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, const size_t* caps, int n,
+                      int offset, int can_udp_gro, int* write_idx) {
+  return push_call(ws, bufs, lens, caps, n, offset, can_udp_gro, false, write_idx);
+}
+
+int wgcs_wstager_push_pinned(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, const size_t* caps,
+                             int n, int offset, int can_udp_gro, int* write_idx) {
+  return push_call(ws, bufs, lens, caps, n, offset, can_udp_gro, true, write_idx);
 }
 
 int wgcs_wstager_submit(wgcs_wstager* ws, uint64_t* batch) {
@@ -331,7 +378,8 @@ int wgcs_wstager_submit(wgcs_wstager* ws, uint64_t* batch) {
     int32_t* d_nw = s.d_res + nd;
     int32_t* d_tw = s.d_res + 2 * (size_t)nd;
     int32_t* d_wlen = s.d_res + 2 * (size_t)nd + np;
-    e = hipMemcpyAsync(s.d_stage, s.h_stage, s.used, hipMemcpyHostToDevice, q);
+    int32_t* d_wpos = s.d_res + 2 * (size_t)nd + 2 * (size_t)np;
+    if (s.used) e = hipMemcpyAsync(s.d_stage, s.h_stage, s.used, hipMemcpyHostToDevice, q);
     if (e == hipSuccess) e = hipMemcpyAsync(s.d_bufs, s.h_bufs, np * sizeof(wgcs_gro_buf), hipMemcpyHostToDevice, q);
     if (e == hipSuccess) e = hipMemcpyAsync(s.d_moves, s.h_moves, np * sizeof(WsMove), hipMemcpyHostToDevice, q);
     if (e == hipSuccess) e = hipMemcpyAsync(s.d_calls, s.h_calls, nd * sizeof(wgcs_gro_call), hipMemcpyHostToDevice, q);
@@ -339,11 +387,12 @@ int wgcs_wstager_submit(wgcs_wstager* ws, uint64_t* batch) {
     if (e == hipSuccess) e = launch_ws_scatter(s.d_stage, s.d_arena, s.d_moves, np, q);
     if (e == hipSuccess) e = launch_gro_batch(s.d_arena, s.d_bufs, s.d_calls, nd, d_status, d_nw, d_tw, q);
     if (e == hipSuccess)
-      e = launch_ws_gather(s.d_arena, s.d_bufs, s.d_calls, s.d_outs, nd, d_status, d_nw, d_tw, d_wlen, s.d_out, q);
+      e = launch_ws_gather(s.d_arena, s.d_bufs, s.d_calls, s.d_outs, nd, d_status, d_nw, d_tw, d_wlen, d_wpos,
+                           s.d_out, q);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(s.h_res, s.d_res, (2 * (size_t)nd + 2 * (size_t)np) * sizeof(int32_t), hipMemcpyDeviceToHost,
+      e = hipMemcpyAsync(s.h_res, s.d_res, (2 * (size_t)nd + 3 * (size_t)np) * sizeof(int32_t), hipMemcpyDeviceToHost,
                          q);
-    if (e == hipSuccess) e = hipMemcpyAsync(s.h_out, s.d_out, s.used, hipMemcpyDeviceToHost, q);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.h_out, s.d_out, s.out_used, hipMemcpyDeviceToHost, q);
   }
   if (e == hipSuccess) e = hipEventRecord(s.done, q);
   if (e != hipSuccess) return hip_fail(ws->ctx, e, "wstager submit");
@@ -393,12 +442,11 @@ int wgcs_wstager_result(wgcs_wstager* ws, uint64_t batch, int write_idx, int* st
   if (nw > 0 && (!to_write || !pkts || !pkt_lens)) return WGCS_ERR_INVALID_ARG;
   const int32_t* tw = s->res_towrite() + c.first;
   const int32_t* wl = s->res_wlen() + c.first;
-  uint64_t pos = c.base;
+  const int32_t* wp = s->res_wpos() + c.first;
   for (int k = 0; k < nw; ++k) {
     to_write[k] = tw[k];
-    pkts[k] = s->h_out + pos + (kHead - kVnet);
+    pkts[k] = s->h_out + c.out_base + (uint32_t)wp[k];
     pkt_lens[k] = (size_t)wl[k];
-    pos += kHead + al16((size_t)wl[k] - kVnet);
   }
   *n_write = nw;
   return WGCS_OK;

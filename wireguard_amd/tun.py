@@ -126,6 +126,16 @@ class Device:
     def sync(self) -> None:
         self._check(self.lib.wgcs_sync(self.h))
 
+    def host_alloc(self, nbytes: int) -> np.ndarray:
+        """Pinned, device-mapped host memory (wgcs_host_alloc) as a uint8 array;
+        release it with host_free(array)."""
+        p = C.c_void_p()
+        self._check(self.lib.wgcs_host_alloc(self.h, nbytes, C.byref(p)))
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(nbytes,))
+
+    def host_free(self, arr: np.ndarray) -> None:
+        self._check(self.lib.wgcs_host_free(self.h, arr.ctypes.data))
+
     # ---------------------------------------------------------- device batch
     def checksum_batch(self, mode: int, arena, pkts, n: int, out, initial=None, inplace: bool = False,
                        stream=None) -> None:
@@ -350,6 +360,18 @@ class WriteStager:
         cc = (C.c_size_t * max(n, 1))(*[len(b) for b in bufs])
         idx = C.c_int(0)
         self.dev._check(self.lib.wgcs_wstager_push(self.h, ptrs, cl, cc, n, offset, int(can_udp_gro), C.byref(idx)))
+        return idx.value
+
+    def push_pinned(self, bufs: list, lens: list, offset: int, can_udp_gro: bool = True) -> int:
+        """Zero-copy push: bufs are numpy views of Device.host_alloc memory,
+        left untouched until this slot's results have been read."""
+        n = len(bufs)
+        ptrs = (C.c_void_p * max(n, 1))(*[b.ctypes.data for b in bufs])
+        cl = (C.c_size_t * max(n, 1))(*lens)
+        cc = (C.c_size_t * max(n, 1))(*[len(b) for b in bufs])
+        idx = C.c_int(0)
+        self.dev._check(self.lib.wgcs_wstager_push_pinned(self.h, ptrs, cl, cc, n, offset, int(can_udp_gro),
+                                                          C.byref(idx)))
         return idx.value
 
     def submit(self) -> int:
