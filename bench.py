@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--no-event-timing", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end measurement")
     ap.add_argument("--push-threads", type=int, default=0,
-                    help="gro_staged: host threads pushing Write calls concurrently (default 1)")
+                    help="gro_staged: host threads pushing Write calls concurrently (default 4)")
     ap.add_argument("--pinned", action="store_true",
                     help="gro_staged: Write buffers in pinned host memory, zero-copy pushes")
     ap.add_argument("--verify", action="store_true", help="check the GPU results against the synth ground truth")

@@ -188,7 +188,7 @@ def run_staged(args, torch, dev, dist, rank, world, local, barrier, calls_per_sl
     # the stager copies outside its lock)
     import concurrent.futures as cf
 
-    threads = max(1, int(getattr(args, "push_threads", 0) or os.environ.get("WGCS_PUSH_THREADS", 1)))
+    threads = max(1, int(getattr(args, "push_threads", 0) or os.environ.get("WGCS_PUSH_THREADS", 4)))
     pool = cf.ThreadPoolExecutor(threads) if threads > 1 else None
     share = [calls_per_slot // threads + (1 if t < calls_per_slot % threads else 0) for t in range(threads)]
 
