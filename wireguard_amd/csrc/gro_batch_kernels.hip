@@ -237,6 +237,73 @@ struct Planner {
     return R_INSERT;
   }
 
+  // The flow's last item, cached in registers for the in-order append fast
+  // path below (it = kNone: nothing cached / no item).
+  struct TailCache {
+    int it, s, tgt, stail, scount;
+    uint32_t l4h, iphit, ipattr, g, nm, seq, psh, slen, cap, valid_s;
+  };
+
+  __device__ void load_tail(TailCache& c, int f) const {
+    c.it = S.fl_tail[f];
+    if (c.it == kNone) return;
+    const int it = c.it;
+    c.s = S.it_slot[it];
+    c.l4h = S.it_l4h[it];
+    c.iphit = S.it_iph[it];
+    c.g = S.it_gso[it];
+    c.nm = S.it_nm[it];
+    c.seq = S.it_seq[it];
+    c.psh = S.it_psh[it];
+    const int s = c.s;
+    c.tgt = S.shead[s];
+    c.slen = S.slen[s];
+    c.cap = S.bcap[S.sbuf[s]];
+    c.valid_s = S.valid[s];
+    c.stail = S.stail[s];
+    c.scount = S.scount[s];
+    c.ipattr = S.ipattr[c.tgt];
+  }
+
+  // tcpGRO when packet bi appends to the flow's last item -- the in-order
+  // bulk case: tcpPacketsCanCoalesce's append branch and coalesceTCPPackets'
+  // checks (gro.go:433-512, :709-734) in the reference's order for that item,
+  // from registers instead of a chain of dependent LDS reads.  Returns false
+  // whenever any of them fails (or TCP options are present), and the general
+  // path (tcp_gro) then decides from LDS exactly as before.
+  __device__ bool tcp_append_fast(TailCache& c, int bi) {
+    if (c.it == kNone) return false;
+    const uint32_t th = S.th[bi], iph = S.iph[bi];
+    if (th != c.l4h || th > 20) return false;
+    if (S.ipattr[bi] != c.ipattr) return false;
+    const uint16_t lhs = (uint16_t)(c.g + (uint16_t)(c.g * c.nm));
+    if (S.seq[bi] != c.seq + (uint32_t)lhs) return false;
+    if (c.psh) return false;
+    const int plen_s = (int)c.slen - offset;
+    if ((plen_s - (int)(iph + th)) % (int)c.g != 0) return false;
+    if (S.gso[bi] > c.g) return false;
+    const int pay = ((int)S.slen[bi] - offset) - (int)(uint8_t)(c.iphit + c.l4h);
+    if ((int)c.cap - offset < plen_s + pay) return false;  // coalesceInsufficientCap
+    if (c.nm == 0 && !c.valid_s) return false;             // coalesceItemInvalidCSum
+    if (!S.valid[bi]) return false;                        // coalescePktInvalidCSum
+    if (S.psh[bi]) {  // pktHead[iphLen+13] |= PSH (gro.go:724-729)
+      S.it_psh[c.it] = 1;
+      S.spsh[c.s] = 1;
+      c.psh = 1;
+    }
+    S.pstart[bi] = (uint16_t)(uint8_t)(c.iphit + c.l4h);
+    S.plen[bi] = (uint16_t)pay;
+    S.pnext[bi] = kNone;
+    S.pnext[c.stail] = (int16_t)bi;
+    c.stail = bi;
+    S.stail[c.s] = (int16_t)bi;
+    S.scount[c.s] = (int16_t)(++c.scount);
+    c.slen += (uint32_t)pay;
+    S.slen[c.s] = c.slen;
+    S.it_nm[c.it] = (uint16_t)(++c.nm);
+    return true;
+  }
+
   // udpGRO (gro.go:971-1095) after its pre-checks
   __device__ int udp_gro(int bi) {
     const int f = S.flow[bi];
@@ -280,9 +347,25 @@ struct Planner {
   // its own flow's, so every flow of a call runs on its own thread.
   __device__ void run_flow(int f) {
     const bool tcp = S.cand[f] <= C_TCP6;
+    TailCache c;
+    c.it = kNone;
+    bool fresh = false;  // c mirrors the flow's last item in LDS
     for (int i = f; i < S.n_eff; ++i) {
       if (S.flow[i] != f || S.cand[i] == C_NOT || S.noop[i]) continue;
-      S.res[i] = (uint8_t)(tcp ? tcp_gro(i) : udp_gro(i));
+      if (!tcp) {
+        S.res[i] = (uint8_t)udp_gro(i);
+        continue;
+      }
+      if (!fresh) {
+        load_tail(c, f);
+        fresh = true;
+      }
+      if (tcp_append_fast(c, i)) {
+        S.res[i] = R_COALESCED;
+        continue;
+      }
+      S.res[i] = (uint8_t)tcp_gro(i);
+      fresh = false;  // inserts, prepends, deletes: reload from LDS
     }
   }
 
