@@ -60,6 +60,7 @@ struct GroSmem {
   int16_t pnext[kMaxB], sbuf[kMaxB], shead[kMaxB], stail[kMaxB];
   int16_t it_slot[kMaxB], it_prev[kMaxB], it_next[kMaxB], fl_head[kMaxB], fl_tail[kMaxB];
   int16_t to_write[kMaxB], scount[kMaxB];
+  int16_t fnext[kMaxB];                 // next packet of the same flow (kNone: last)
   // materializations (<= n: one per final item or per prepend, each the
   // work of a distinct packet); m_item: -1 = plain
   int16_t m_buf[kMaxB], m_first[kMaxB], m_count[kMaxB], m_item[kMaxB];
@@ -350,8 +351,8 @@ struct Planner {
     TailCache c;
     c.it = kNone;
     bool fresh = false;  // c mirrors the flow's last item in LDS
-    for (int i = f; i < S.n_eff; ++i) {
-      if (S.flow[i] != f || S.cand[i] == C_NOT || S.noop[i]) continue;
+    for (int i = f, nx; i != kNone; i = nx) {  // the flow's packets in order (fnext links)
+      nx = S.fnext[i];
       if (!tcp) {
         S.res[i] = (uint8_t)udp_gro(i);
         continue;
@@ -635,6 +636,19 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
       }
     }
     S.flow[t] = (uint16_t)f;
+    // and the next later packet of the same flow, so the flow's thread walks
+    // only its own packets (each thread searches for its own link in parallel)
+    int nx = kNone;
+    for (int q = t + 1; q < n_eff; ++q) {
+      if (S.keyh[q] != kh || S.cand[q] != c || S.noop[q]) continue;
+      bool eq = true;
+      for (int w = 0; w < nkw; ++w) eq = eq && S.kw[q][w] == S.kw[t][w];
+      if (eq) {
+        nx = q;
+        break;
+      }
+    }
+    S.fnext[t] = (int16_t)nx;
   }
   // checksumValid of every candidate: one 16-lane row per packet
   for (int p = row; p < n_eff; p += 16) {  // row-uniform
