@@ -253,11 +253,11 @@ int push_call(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, 
       c.status = WGCS_ERR_INVALID_OFFSET;
       break;
     }
-  size_t need = 0, need_out = 0;
+  size_t need = 0, need_out = 0, total = 0;
   if (!c.status)
     for (int i = 0; i < n; ++i) {
-      if (caps[i] < lens[i] || caps[i] > 0xFFFFFFFFull)
-        return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: cap(bufs[%d]) < len or >= 4 GiB", i);
+      if (caps[i] < lens[i]) return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: cap(bufs[%d]) < len", i);
+      total += lens[i] - offset;
       if (pinned && !host_mapped(ws->ctx, bufs[i] + offset - kVnet, lens[i] - offset + kVnet))
         return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: bufs[%d] is not in wgcs_host_alloc memory", i);
       if (!pinned) need += kHead + al16(lens[i] - offset);
@@ -286,13 +286,17 @@ int push_call(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, 
     at = s.used;
     for (int i = 0; i < n; ++i) {
       const size_t pl = lens[i] - (size_t)offset;
+      // The device slice's capacity: a coalesced buffer never holds more than
+      // all of the call's packets, so capping cap there changes no capacity
+      // check of handleGRO (gro.go:685-688, :730-733) and bounds the arena.
+      const size_t cap = std::min(caps[i], (size_t)offset + total);
       const uintptr_t hp = (uintptr_t)(bufs[i] + offset);  // the packet in host memory
       const uint64_t phase = pinned ? (uint64_t)(hp & 15u) : 0u;
       const uint64_t pkt = s.arena + 32 + al16((size_t)offset) + phase;  // the packet in the arena
       wgcs_gro_buf& b = s.h_bufs[s.npk];
       b.off = pkt - (uint64_t)offset;
       b.len = (uint32_t)lens[i];
-      b.cap = (uint32_t)caps[i];
+      b.cap = (uint32_t)cap;
       WsMove& m = s.h_moves[s.npk];
       if (pinned) {  // the aligned chunks holding bufs[i][offset-10:len], read over PCIe
         const uintptr_t c0 = (hp - kVnet) & ~(uintptr_t)15, c1 = (hp + pl + 15) & ~(uintptr_t)15;
@@ -307,7 +311,7 @@ int push_call(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, 
         m.flags = 0;
         s.used += kHead + al16(pl);
       }
-      s.arena += arena_need((size_t)offset, caps[i]);
+      s.arena += arena_need((size_t)offset, cap);
       ++s.npk;
     }
     s.out_used += need_out;
