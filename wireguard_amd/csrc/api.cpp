@@ -57,6 +57,15 @@ int ensure_pinned(wgcs_ctx* ctx, HostBuf& b, size_t bytes) {
   size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
   hipError_t e = hipHostMalloc(&b.ptr, want, hipHostMallocDefault);
   if (e != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc");
+  // kernels take pinned staging pointers as they are (zero-copy per-call paths)
+  void* d = nullptr;
+  e = hipHostGetDevicePointer(&d, b.ptr, 0);
+  if (e != hipSuccess || d != b.ptr) {
+    hipHostFree(b.ptr);
+    b.ptr = nullptr;
+    return e != hipSuccess ? hip_fail(ctx, e, "hipHostGetDevicePointer")
+                           : set_err(ctx, WGCS_ERR_HIP, "pinned memory is not mapped at its host address");
+  }
   b.cap = want;
   return WGCS_OK;
 }

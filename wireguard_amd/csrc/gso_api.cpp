@@ -26,14 +26,15 @@ struct GsoResult {
 };
 
 // Runs one job through the kernel and copies its segments into bufs.
-// vbuf = [10-byte virtio header | packet bytes] in host memory.  One round
-// trip: the segments land in a packed device region whose size the host
-// bounds from the virtio header (gso_out_layout), so the D2H of the segments
-// is queued with the launch instead of after a read-back of their sizes.
+// vbuf = [10-byte virtio header | packet bytes] in the context's pinned
+// staging.  Zero-copy round trip: the kernel reads the job, its descriptor and
+// the super-packet straight from pinned host memory over PCIe and writes the
+// segments (into a packed region whose size the host bounds from the virtio
+// header, gso_out_layout), their sizes, the count and the status straight
+// back into pinned host memory -- one launch and one wait, no copy commands.
 // The room checks use bufs[0]'s room, as the reference does (tun/tun.go:546,
 // gro.go:1406-1410); other buffers are checked when copying, where the Go
-// code would panic on the slice.  Caller holds ctx->mu (vbuf may be the
-// context's own pinned staging).
+// code would panic on the slice.  Caller holds ctx->mu.
 int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflags, uint8_t* const* bufs,
                  const size_t* buf_lens, int nbufs, int* sizes, int offset, GsoResult* res) {
   if (nbufs <= 0 || !bufs || !buf_lens || !sizes || offset < 0)
@@ -56,11 +57,9 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   const bool stale_id = (raw || gtype != 0) && v4 && cs <= 5 && region;
   hipSetDevice(ctx->device);
   int rc;
-  const size_t meta = (size_t)nbufs * 4 + 16;  // sizes[nbufs] | count | status
+  const size_t meta = ((size_t)nbufs * 4 + 16 + 15) & ~(size_t)15;  // sizes[nbufs] | count | status
   const size_t aux = sizeof(wgcs_gso_job) + sizeof(GsoOutPos);
-  if ((rc = ensure_dev(ctx, ctx->d_arena, vlen + 32)) || (rc = ensure_dev(ctx, ctx->d_aux, aux)) ||
-      (rc = ensure_dev(ctx, ctx->d_out, region + 16)) || (rc = ensure_dev(ctx, ctx->d_out2, meta)) ||
-      (rc = ensure_pinned(ctx, ctx->h_meta, meta + aux)) || (rc = ensure_pinned(ctx, ctx->h_stage, region + 16)))
+  if ((rc = ensure_pinned(ctx, ctx->h_meta, meta + aux)) || (rc = ensure_pinned(ctx, ctx->h_stage, region + 16)))
     return rc;
   hipStream_t s = ctx->stream;
   uint8_t* hm = (uint8_t*)ctx->h_meta.ptr;
@@ -72,28 +71,19 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   hpos->base = 0;
   hpos->pitch = pitch;
   hpos->pad = 0;
-  int32_t* d_sizes = (int32_t*)ctx->d_out2.ptr;
-  int32_t* d_count = d_sizes + nbufs;
-  int32_t* d_status = d_count + 1;
-  hipError_t e = hipMemcpyAsync(ctx->d_arena.ptr, vbuf, vlen, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(ctx->d_aux.ptr, hjob, aux, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && stale_id) {
-    uint8_t* hs = (uint8_t*)ctx->h_stage.ptr;
+  int32_t* h = (int32_t*)hm;
+  uint8_t* hs = (uint8_t*)ctx->h_stage.ptr;
+  if (stale_id) {
     memset(hs, 0, region);
     for (uint32_t i = 0; i < nseg_bound && i < (uint32_t)nbufs; ++i)
       if (buf_lens[i] > (size_t)offset) memcpy(hs + (size_t)i * pitch, bufs[i] + offset, std::min<size_t>(6, buf_lens[i] - offset));
-    e = hipMemcpyAsync(ctx->d_out.ptr, hs, region, hipMemcpyHostToDevice, s);
   }
-  if (e != hipSuccess) return hip_fail(ctx, e, "H2D");
-  e = launch_gso_split_batch((const uint8_t*)ctx->d_arena.ptr, (const wgcs_gso_job*)ctx->d_aux.ptr, 1,
-                             (uint8_t*)ctx->d_out.ptr, 0, 0, (uint32_t)nbufs, d_sizes, d_count, d_status, s,
-                             (const GsoOutPos*)((uint8_t*)ctx->d_aux.ptr + sizeof(wgcs_gso_job)), (uint32_t)room);
+  // pinned staging is mapped into the device's address space at its host
+  // address (checked by ensure_pinned's hipHostMalloc contract, see api.cpp)
+  hipError_t e = launch_gso_split_batch(vbuf, hjob, 1, hs, 0, 0, (uint32_t)nbufs, h, h + nbufs, h + nbufs + 1, s,
+                                        hpos, (uint32_t)room);
   if (e != hipSuccess) return hip_fail(ctx, e, "gso_split launch");
-  int32_t* h = (int32_t*)hm;
-  e = hipMemcpyAsync(h, d_sizes, meta, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess && region) e = hipMemcpyAsync(ctx->h_stage.ptr, ctx->d_out.ptr, region, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "gso_split wait");
   res->count = h[nbufs];
   res->status = h[nbufs + 1];
   if (res->status != 0 && res->status != WGCS_ERR_TOO_MANY_SEGMENTS) {
@@ -110,7 +100,7 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
       res->count = i;
       return WGCS_OK;
     }
-    memcpy(bufs[i] + offset, (const uint8_t*)ctx->h_stage.ptr + (size_t)i * pitch, (size_t)h[i]);
+    memcpy(bufs[i] + offset, hs + (size_t)i * pitch, (size_t)h[i]);
   }
   return WGCS_OK;
 }
@@ -172,7 +162,10 @@ int wgcs_handle_virtio_read(wgcs_ctx* ctx, uint8_t* read_buf, size_t n, uint8_t*
   *n_out = 0;
   GsoResult r;
   std::lock_guard<std::mutex> g(ctx->mu);
-  int rc = run_gso_host(ctx, read_buf, n, 0, bufs, buf_lens, nbufs, sizes, offset, &r);
+  int rc;
+  if ((rc = ensure_pinned(ctx, ctx->h_out, n + 16))) return rc;
+  if (n) memcpy(ctx->h_out.ptr, read_buf, n);  // the kernel reads it from pinned memory
+  rc = run_gso_host(ctx, (const uint8_t*)ctx->h_out.ptr, n, 0, bufs, buf_lens, nbufs, sizes, offset, &r);
   if (rc) return rc;
   if (n >= 10 && (r.status == 0 || r.status == WGCS_ERR_TOO_MANY_SEGMENTS)) {
     uint8_t* rb = read_buf + 10;
