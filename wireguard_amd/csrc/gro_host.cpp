@@ -1,8 +1,9 @@
 // gro_host.cpp -- handleGRO (/root/reference/tun/gro.go:1326-1367) behind the
 // C ABI, MI355X-first:
-//   1. the candidate packets are gathered once into the pinned staging ring
-//      and copied to HBM; checksumValid (gro.go:554-612) for every candidate
-//      is computed there by the batch VALIDATE kernel.  Validation always
+//   1. the candidate packets are gathered once into pinned staging, which
+//      the kernels read over PCIe (no copy commands); checksumValid
+//      (gro.go:554-612) for every candidate is computed by the batch VALIDATE
+//      kernel.  Validation always
 //      precedes mutation in the reference (gro.go:665-681, :709-723,
 //      :767-775), so precomputed validity bits are exact.  The plan (2) is
 //      made first assuming valid checksums and queued with the VALIDATE
@@ -14,8 +15,8 @@
 //      plan per output buffer.
 //   3. the GPU coalesce kernel (gro_kernels.hip) builds every merged
 //      super-packet (payload gather + applyTCPCoalesce/applyUDPCoalesce
-//      header rewrite + virtio header), and the results are copied back
-//      into the caller's buffers.
+//      header rewrite + virtio header) into pinned staging, and the results
+//      are copied into the caller's buffers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -35,22 +36,22 @@ namespace {
 
 using namespace wgcs::gro;
 
-// Queue the coalesce plan on stream s: H2D of items + pieces, kernel, D2H.
+// Queue the coalesce plan on stream s, zero-copy: the kernel reads the staged
+// packets, the items and the pieces from pinned host memory and writes the
+// super-packets into pinned host memory (pinned staging is mapped into the
+// device's address space at its host address, checked by ensure_pinned).
 int queue_coalesce(wgcs_ctx* ctx, const Plan& pl, hipStream_t s) {
   if (pl.items.empty()) return WGCS_OK;
   const size_t ib = pl.items.size() * sizeof(GroItem), sb = std::max<size_t>(pl.segs.size(), 1) * sizeof(GroSeg);
   int rc;
-  if ((rc = ensure_pinned(ctx, ctx->h_meta, ib + sb)) || (rc = ensure_dev(ctx, ctx->d_aux, ib + sb)) ||
-      (rc = ensure_dev(ctx, ctx->d_out, pl.out_bytes + 16)) || (rc = ensure_pinned(ctx, ctx->h_out, pl.out_bytes + 16)))
+  if ((rc = ensure_pinned(ctx, ctx->h_meta, ib + sb)) || (rc = ensure_pinned(ctx, ctx->h_out, pl.out_bytes + 16)))
     return rc;
   memcpy(ctx->h_meta.ptr, pl.items.data(), ib);
   memcpy((uint8_t*)ctx->h_meta.ptr + ib, pl.segs.data(), pl.segs.size() * sizeof(GroSeg));
-  hipError_t e = hipMemcpyAsync(ctx->d_aux.ptr, ctx->h_meta.ptr, ib + sb, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess)
-    e = launch_gro_coalesce((const uint8_t*)ctx->d_arena.ptr, (const GroItem*)ctx->d_aux.ptr,
-                            (uint32_t)pl.items.size(), (const GroSeg*)((uint8_t*)ctx->d_aux.ptr + ib),
-                            (uint32_t)pl.segs.size(), (uint8_t*)ctx->d_out.ptr, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(ctx->h_out.ptr, ctx->d_out.ptr, pl.out_bytes, hipMemcpyDeviceToHost, s);
+  const hipError_t e =
+      launch_gro_coalesce((const uint8_t*)ctx->h_stage.ptr, (const GroItem*)ctx->h_meta.ptr, (uint32_t)pl.items.size(),
+                          (const GroSeg*)((uint8_t*)ctx->h_meta.ptr + ib), (uint32_t)pl.segs.size(),
+                          (uint8_t*)ctx->h_out.ptr, s);
   return e == hipSuccess ? WGCS_OK : hip_fail(ctx, e, "GRO coalesce");
 }
 
@@ -108,14 +109,14 @@ extern "C" int wgcs_handle_gro(wgcs_ctx* ctx, uint8_t** bufs, size_t* lens, size
   int rc;
   std::vector<uint8_t> real(n, 0);
   if (ncand) {
-    // ---- one submission: stage candidates, VALIDATE, coalesce (speculative plan), D2H
+    // ---- one submission: stage candidates (pinned), VALIDATE, coalesce
+    // (speculative plan); the kernels read and write pinned host memory
+    // directly, so there is no copy command, one wait
     const size_t meta = (size_t)ncand * sizeof(wgcs_pkt);
-    if ((rc = ensure_pinned(ctx, ctx->h_stage, stage_bytes + 16 + meta + ncand)) ||
-        (rc = ensure_dev(ctx, ctx->d_arena, stage_bytes + 16)) || (rc = ensure_dev(ctx, ctx->d_pkts, meta)) ||
-        (rc = ensure_dev(ctx, ctx->d_init, ncand)))
-      return rc;
+    const size_t stage_al = (stage_bytes + 15) & ~(size_t)15;
+    if ((rc = ensure_pinned(ctx, ctx->h_stage, stage_al + 16 + meta + ncand + 16))) return rc;
     uint8_t* hs = (uint8_t*)ctx->h_stage.ptr;
-    wgcs_pkt* hp = (wgcs_pkt*)(hs + ((stage_bytes + 15) & ~(size_t)15));
+    wgcs_pkt* hp = (wgcs_pkt*)(hs + stage_al + 16);
     uint8_t* hv = (uint8_t*)(hp + ncand);
     std::vector<int> cidx;
     cidx.reserve(ncand);
@@ -129,12 +130,7 @@ extern "C" int wgcs_handle_gro(wgcs_ctx* ctx, uint8_t** bufs, size_t* lens, size
                    (uint8_t)(udp ? 17 : 6), (uint8_t)(v6 ? WGCS_PKT_V6 : 0));
       cidx.push_back(i);
     }
-    hipError_t e = hipMemcpyAsync(ctx->d_arena.ptr, hs, stage_bytes, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(ctx->d_pkts.ptr, hp, meta, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess)
-      e = launch_checksum_batch(WGCS_MODE_VALIDATE, 0, (uint8_t*)ctx->d_arena.ptr, (const wgcs_pkt*)ctx->d_pkts.ptr,
-                                nullptr, ncand, ctx->d_init.ptr, s, ctx->num_cu, ctx->tune);
-    if (e == hipSuccess) e = hipMemcpyAsync(hv, ctx->d_init.ptr, ncand, hipMemcpyDeviceToHost, s);
+    hipError_t e = launch_checksum_batch(WGCS_MODE_VALIDATE, 0, hs, hp, nullptr, ncand, hv, s, ctx->num_cu, ctx->tune);
     if (e != hipSuccess) return hip_fail(ctx, e, "GRO validate");
     if ((rc = queue_coalesce(ctx, pl, s))) return rc;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "GRO sync");
@@ -162,7 +158,7 @@ extern "C" int wgcs_handle_gro(wgcs_ctx* ctx, uint8_t** bufs, size_t* lens, size
     const int slot = pl.item_slot[k];
     const GroItem& it = pl.items[k];
     if (it.kind & GRO_KIND_RAW)
-      memcpy(bufs[slot] + offset, (uint8_t*)ctx->h_out.ptr + it.out_off + kVnetLen, it.pkt_len);
+      memcpy(bufs[slot] + offset, (uint8_t*)ctx->h_out.ptr + it.out_off + kVnetLen, it.pkt_len);  // RAW item
     else
       memcpy(bufs[slot] + offset - kVnetLen, (uint8_t*)ctx->h_out.ptr + it.out_off, kVnetLen + it.pkt_len);
   }

@@ -4,7 +4,7 @@
 // packets (tun/tun.go:654-700 -> gro.go:1326-1367), then one write(2) per
 // toWrite entry of bufs[i][offset-10:] (tun.go:687-698); it is called from
 // every peer's RoutineSendToInternet (device/receive.go:483-498).  One such
-// call is far too small for a GPU round trip (wgcs_handle_gro: ~70 us), so the
+// call is far too small for a GPU round trip (wgcs_handle_gro: ~55 us), so the
 // write stager aggregates many Write calls into one pinned ring slot and runs
 // all of handleGRO on the GPU, one workgroup per call (gro_batch_kernels.hip):
 //
