@@ -239,6 +239,10 @@ int wgcs_checksum_batch(wgcs_ctx* ctx, int mode, unsigned flags, uint8_t* d_aren
   return e == hipSuccess ? WGCS_OK : hip_fail(ctx, e, "checksum_batch launch");
 }
 
+// Host batches up to this size run zero-copy (the kernel reads pinned staging
+// over PCIe); larger ones go through copy-engine H2D / D2H.
+constexpr size_t kZeroCopyMax = 1u << 20;
+
 int wgcs_checksum_batch_host(wgcs_ctx* ctx, int mode, unsigned flags, uint8_t* h_arena, size_t arena_len,
                              const wgcs_pkt* h_pkts, const uint64_t* h_initial, uint32_t n, void* h_out) {
   if (!ctx) return WGCS_ERR_INVALID_ARG;
@@ -254,10 +258,33 @@ int wgcs_checksum_batch_host(wgcs_ctx* ctx, int mode, unsigned flags, uint8_t* h
   hipSetDevice(ctx->device);
   const size_t out_bytes = (size_t)n * (mode == WGCS_MODE_VALIDATE ? 1 : 2);
   int rc;
+  const bool fold_init = h_initial && mode == WGCS_MODE_FOLD;
+  if (arena_len <= kZeroCopyMax) {
+    // Small batches (the per-call entry points: one packet or one read):
+    // zero-copy through pinned staging -- the kernel reads the packets and
+    // descriptors and writes its results over PCIe; one launch, one wait, no
+    // copy commands (their fixed costs dominate at this size).
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t o_pk = al(arena_len) + 16, o_in = o_pk + al(n * sizeof(wgcs_pkt)),
+                 o_out = o_in + (fold_init ? al(n * sizeof(uint64_t)) : 0);
+    if ((rc = ensure_pinned(ctx, ctx->h_stage, o_out + al(out_bytes) + 16))) return rc;
+    uint8_t* hs = (uint8_t*)ctx->h_stage.ptr;
+    if (arena_len) memcpy(hs, h_arena, arena_len);
+    memcpy(hs + o_pk, h_pkts, n * sizeof(wgcs_pkt));
+    if (fold_init) memcpy(hs + o_in, h_initial, n * sizeof(uint64_t));
+    hipError_t e = launch_checksum_batch(mode, flags, hs, (const wgcs_pkt*)(hs + o_pk),
+                                         fold_init ? (const uint64_t*)(hs + o_in) : nullptr, n, hs + o_out,
+                                         ctx->stream, ctx->num_cu, ctx->tune);
+    if (e != hipSuccess) return hip_fail(ctx, e, "checksum_batch launch");
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return hip_fail(ctx, e, "checksum_batch wait");
+    memcpy(h_out, hs + o_out, out_bytes);
+    if ((flags & WGCS_F_INPLACE) && arena_len) memcpy(h_arena, hs, arena_len);
+    return WGCS_OK;
+  }
   if ((rc = ensure_dev(ctx, ctx->d_arena, arena_len + 16)) || (rc = ensure_dev(ctx, ctx->d_pkts, n * sizeof(wgcs_pkt))) ||
       (rc = ensure_dev(ctx, ctx->d_out, out_bytes)))
     return rc;
-  if (h_initial && mode == WGCS_MODE_FOLD && (rc = ensure_dev(ctx, ctx->d_init, n * sizeof(uint64_t)))) return rc;
+  if (fold_init && (rc = ensure_dev(ctx, ctx->d_init, n * sizeof(uint64_t)))) return rc;
   hipStream_t s = ctx->stream;
   hipError_t e = hipMemcpyAsync(ctx->d_arena.ptr, h_arena, arena_len, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(ctx->d_pkts.ptr, h_pkts, n * sizeof(wgcs_pkt), hipMemcpyHostToDevice, s);
