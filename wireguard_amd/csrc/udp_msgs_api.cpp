@@ -122,9 +122,9 @@ int wgcs_coalesce_messages_batch(wgcs_ctx* ctx, uint8_t* d_bufs, uint64_t buf_st
 }
 
 // splitMessages(msgs, firstMsgAt) (nPackets, err) -- conn/bind.go:542-597.
-// One round trip: the source messages go up in one copy, the packets come back
-// in a packed region whose pitch (the largest packet) the host knows from the
-// (N, gsoSize) pairs.
+// One round trip: the source messages are staged in pinned memory, the packets
+// land in a packed pinned region whose pitch (the largest packet) the host
+// knows from the (N, gsoSize) pairs; the kernel reads and writes both over PCIe.
 int wgcs_split_messages(wgcs_ctx* ctx, uint8_t* const* bufs, size_t buf_len, int* ns, const uint8_t* const* oobs,
                         const size_t* nns, int n_msgs, int first_msg_at, int* addr_src, int* n_packets) {
   if (!ctx || !n_packets) return WGCS_ERR_INVALID_ARG;
@@ -160,11 +160,13 @@ int wgcs_split_messages(wgcs_ctx* ctx, uint8_t* const* bufs, size_t buf_len, int
   std::lock_guard<std::mutex> g(ctx->mu);
   hipSetDevice(ctx->device);
   int rc;
-  if ((rc = ensure_dev(ctx, ctx->d_arena, in_bytes + 16)) || (rc = ensure_dev(ctx, ctx->d_out, out_bytes + 16)) ||
-      (rc = ensure_dev(ctx, ctx->d_aux, meta)) || (rc = ensure_pinned(ctx, ctx->h_stage, std::max(in_bytes, out_bytes) + 16)) ||
+  // zero-copy: the kernel reads the messages and writes the packets through
+  // pinned staging over PCIe (one launch, one wait, no copy commands)
+  if ((rc = ensure_pinned(ctx, ctx->h_stage, in_bytes + 16)) || (rc = ensure_pinned(ctx, ctx->h_out, out_bytes + 16)) ||
       (rc = ensure_pinned(ctx, ctx->h_meta, meta)))
     return rc;
   uint8_t* hs = (uint8_t*)ctx->h_stage.ptr;
+  uint8_t* ho = (uint8_t*)ctx->h_out.ptr;
   for (int t = 0; t < nsrc; ++t) {
     const int i = first_msg_at + t;
     const size_t n = (size_t)std::max(ns[i], 0), gs = gso[i] > 0 ? (size_t)gso[i] : 0;
@@ -176,28 +178,19 @@ int wgcs_split_messages(wgcs_ctx* ctx, uint8_t* const* bufs, size_t buf_len, int
     hm[i] = ns[i];
     hm[n_msgs + i] = gso[i];
   }
-  int32_t* dm = (int32_t*)ctx->d_aux.ptr;
   hipStream_t s = ctx->stream;
-  hipError_t e = hipSuccess;
-  if (in_bytes) e = hipMemcpyAsync(ctx->d_arena.ptr, hs, in_bytes, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(dm, hm, (size_t)n_msgs * 8, hipMemcpyHostToDevice, s);
-  if (e != hipSuccess) return hip_fail(ctx, e, "H2D");
-  const uint8_t* d_in = (const uint8_t*)ctx->d_arena.ptr;  // source i at (i - first) * in_stride
-  int32_t* d_nout = dm + 2 * n_msgs;
-  int32_t* d_src = dm + 3 * n_msgs;
-  int32_t* d_cs = dm + 4 * n_msgs;  // count, status
-  e = launch_udp_split(d_in, in_stride, (uint32_t)buf_len, dm, dm + n_msgs, (uint32_t)n_msgs, (uint32_t)first_msg_at,
-                       1, (uint8_t*)ctx->d_out.ptr, out_stride, d_nout, d_src, d_cs, d_cs + 1, s);
+  int32_t* h_nout = hm + 2 * n_msgs;
+  int32_t* h_src = hm + 3 * n_msgs;
+  int32_t* h_cs = hm + 4 * n_msgs;  // count, status
+  hipError_t e = launch_udp_split(hs, in_stride, (uint32_t)buf_len, hm, hm + n_msgs, (uint32_t)n_msgs,
+                                  (uint32_t)first_msg_at, 1, ho, out_stride, h_nout, h_src, h_cs, h_cs + 1, s);
   if (e != hipSuccess) return hip_fail(ctx, e, "split_messages launch");
-  e = hipMemcpyAsync(hm + 2 * n_msgs, d_nout, (size_t)n_msgs * 8 + 8, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess && out_bytes) e = hipMemcpyAsync(hs, ctx->d_out.ptr, out_bytes, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return hip_fail(ctx, e, "D2H");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "split_messages wait");
   const int count = hm[4 * n_msgs], status = hm[4 * n_msgs + 1];
   for (int k = 0; k < n_msgs; ++k) {
     const int nk = hm[2 * n_msgs + k];
     if (k < count) {
-      memcpy(bufs[k], hs + (size_t)k * out_stride, (size_t)nk);
+      memcpy(bufs[k], ho + (size_t)k * out_stride, (size_t)nk);
       addr_src[k] = hm[3 * n_msgs + k];
     } else {
       addr_src[k] = k;
@@ -209,9 +202,9 @@ int wgcs_split_messages(wgcs_ctx* ctx, uint8_t* const* bufs, size_t buf_len, int
 }
 
 // coalesceMessages(msgs, bufs, endpoint, addr) nMsgs -- conn/bind.go:599-662.
-// The buffers go up into 64 KiB device slots (one pitched copy of their
-// lengths), the kernel plans and appends in place, and each message's
-// appended bytes come back into its first buffer's spare capacity.
+// The buffers are staged into 64 KiB slots of pinned memory, the kernel plans
+// and appends in place there (over PCIe), and each message's appended bytes
+// are copied into its first buffer's spare capacity.
 int wgcs_coalesce_messages(wgcs_ctx* ctx, uint8_t* const* bufs, const size_t* lens, const size_t* caps, int nbufs,
                            int dst_is_v6, const uint8_t* src_ctl, size_t src_len, uint8_t* const* oobs,
                            size_t* oob_lens, const size_t* oob_caps, int* msg_first, size_t* msg_len, int* n_msgs) {
@@ -221,20 +214,18 @@ int wgcs_coalesce_messages(wgcs_ctx* ctx, uint8_t* const* bufs, const size_t* le
   if (!bufs || !lens || !caps || !msg_first || !msg_len || (oobs && (!oob_lens || !oob_caps)) ||
       (src_len && !src_ctl))
     return set_err(ctx, WGCS_ERR_INVALID_ARG, "bufs/lens/caps/msg arrays");
-  size_t wmax = 16;
   for (int j = 0; j < nbufs; ++j) {
     if (lens[j] > caps[j] || lens[j] > 0x7FFFFFFFu) return set_err(ctx, WGCS_ERR_INVALID_ARG, "len(bufs[%d]) > cap", j);
     if (lens[j] > kSlot) return set_err(ctx, WGCS_ERR_INVALID_ARG, "bufs[%d] longer than 64 KiB", j);
-    wmax = std::max(wmax, lens[j]);
   }
   const size_t data = (size_t)nbufs * kSlot;
   const size_t meta = (size_t)nbufs * 4 * 5 + 16;  // lens | caps | first | len | gso | nbufs | n_msgs
   std::lock_guard<std::mutex> g(ctx->mu);
   hipSetDevice(ctx->device);
   int rc;
-  if ((rc = ensure_dev(ctx, ctx->d_arena, data)) || (rc = ensure_dev(ctx, ctx->d_aux, meta)) ||
-      (rc = ensure_pinned(ctx, ctx->h_stage, data)) || (rc = ensure_pinned(ctx, ctx->h_meta, meta)))
-    return rc;
+  // zero-copy: the kernel plans and appends in place in 64 KiB slots of
+  // pinned staging, over PCIe (one launch, one wait, no copy commands)
+  if ((rc = ensure_pinned(ctx, ctx->h_stage, data)) || (rc = ensure_pinned(ctx, ctx->h_meta, meta))) return rc;
   uint8_t* hs = (uint8_t*)ctx->h_stage.ptr;
   int32_t* hm = (int32_t*)ctx->h_meta.ptr;
   for (int j = 0; j < nbufs; ++j) {
@@ -243,29 +234,13 @@ int wgcs_coalesce_messages(wgcs_ctx* ctx, uint8_t* const* bufs, const size_t* le
     hm[nbufs + j] = (int32_t)std::min(caps[j], kSlot);  // exact: appends stop at maxPayloadLen < 64 KiB
   }
   hm[5 * nbufs] = nbufs;
-  int32_t* dm = (int32_t*)ctx->d_aux.ptr;
   hipStream_t s = ctx->stream;
-  hipError_t e = hipMemcpy2DAsync(ctx->d_arena.ptr, kSlot, hs, kSlot, align16(wmax), (size_t)nbufs,
-                                  hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(dm, hm, meta, hipMemcpyHostToDevice, s);
-  if (e != hipSuccess) return hip_fail(ctx, e, "H2D");
-  e = launch_udp_coalesce((uint8_t*)ctx->d_arena.ptr, kSlot, (uint32_t)kSlot, dm + nbufs, dm, dm + 5 * nbufs,
-                          (uint32_t)nbufs, 1, dst_is_v6, dm + 5 * nbufs + 1, dm + 2 * nbufs, dm + 3 * nbufs,
-                          dm + 4 * nbufs, s);
+  hipError_t e = launch_udp_coalesce(hs, kSlot, (uint32_t)kSlot, hm + nbufs, hm, hm + 5 * nbufs, (uint32_t)nbufs, 1,
+                                     dst_is_v6, hm + 5 * nbufs + 1, hm + 2 * nbufs, hm + 3 * nbufs, hm + 4 * nbufs, s);
   if (e != hipSuccess) return hip_fail(ctx, e, "coalesce_messages launch");
-  e = hipMemcpyAsync(hm + 2 * nbufs, dm + 2 * nbufs, (size_t)nbufs * 12 + 8, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return hip_fail(ctx, e, "D2H meta");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "coalesce_messages wait");
   const int nm = hm[5 * nbufs + 1];
   if (nm < 0 || nm > nbufs) return set_err(ctx, WGCS_ERR_HIP, "coalesce kernel returned %d messages", nm);
-  for (int m = 0; m < nm; ++m) {  // appended bytes of message m: [len(first), msg_len) of its first buffer
-    const int f = hm[2 * nbufs + m];
-    const size_t l0 = lens[f], l = (size_t)hm[3 * nbufs + m];
-    if (l > l0) e = hipMemcpyAsync(hs + (size_t)f * kSlot + l0, (uint8_t*)ctx->d_arena.ptr + (size_t)f * kSlot + l0,
-                                   l - l0, hipMemcpyDeviceToHost, s);
-    if (e != hipSuccess) return hip_fail(ctx, e, "D2H");
-  }
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "D2H");
   for (int m = 0; m < nm; ++m) {
     const int f = hm[2 * nbufs + m];
     const size_t l0 = lens[f], l = (size_t)hm[3 * nbufs + m];
