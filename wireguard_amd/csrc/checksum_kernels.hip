@@ -82,6 +82,22 @@ __device__ __forceinline__ Desc unpack(const uint4& d) {
 // chunks that are summed unmasked: lanes stream interior chunk
 // c = c_lo + sub + G*(u + U*it), so one wave instruction reads 64/G
 // contiguous 16*G-byte runs, and each lane owns at most a few edge chunks.
+// The wave's first PPW consecutive descriptors through the scalar path (the
+// address is wave-uniform, so these are s_load_dwordx4: no TA/TD round trip
+// before the first frame load); each group picks its own.  Later descriptors
+// are prefetched with vector loads, which the frame loads do not wait on.
+template <int PPW>
+__device__ __forceinline__ uint4 wave_desc(const uint4* __restrict__ pkts, uint32_t base, uint32_t n, int grp) {
+  uint4 d[PPW];
+#pragma unroll
+  for (int k = 0; k < PPW; ++k) d[k] = (base + (uint32_t)k < n) ? pkts[base + k] : make_uint4(0, 0, 0, 0);
+  uint4 r = d[0];
+#pragma unroll
+  for (int k = 1; k < PPW; ++k)
+    if (grp == k) r = d[k];
+  return r;
+}
+
 template <int MODE, int G, int U, bool NT>
 __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict__ arena,
                                                              const uint4* __restrict__ pkts,
@@ -101,16 +117,12 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
   if (xcd) blk = (blk & 7u) * (gridDim.x >> 3) + (blk >> 3);
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blk * (blockDim.x >> 6) + (threadIdx.x >> 6)));
   const uint32_t step = gridDim.x * (blockDim.x >> 6) * PPW;
-  uint4 dn = make_uint4(0, 0, 0, 0);
-  {
-    const uint32_t p0 = wave * PPW + grp;
-    if (p0 < n) dn = pkts[p0];
-  }
+  uint4 dn = wave_desc<PPW>(pkts, wave * PPW, n, grp);
   for (uint32_t base = wave * PPW; base < n; base += step) {  // wave-uniform loop
     const uint32_t p = base + grp;
     const bool active = p < n;
     const Desc d = unpack(dn);
-    if (p + step < n) dn = pkts[p + step];  // prefetch the next descriptor
+    if (p + step < n) dn = pkts[p + step];  // prefetch the next descriptor (vector: waited on by vmcnt only)
     uint8_t* pkt = arena + d.off;
     const int len = active ? d.len : 0;
     const int cs = d.cs;
