@@ -194,10 +194,17 @@ def main():
         el = time.perf_counter() - t0
         return el, (e0.elapsed_time(e1) / K if use_events else None)
 
+    # The one-stream reference runs before the timed region: measured after a
+    # two-stream burst, the same launches read ~2-3 us slower per launch than
+    # in a one-stream process (profiles/r2_probe_iso_order.txt); `value` and
+    # kernel_ms come from the timed two-stream region either way.
+    iso_first = os.environ.get("WGCS_ISO_FIRST", "1") == "1"
+    iso_ms = None
+    if use_events and S > 1 and iso_first:
+        _, iso_ms = timed(max(args.steps, 20), args.warmup, 1)
     elapsed, kern_ms = timed(args.steps, args.warmup, S)
     elapsed = shard.max_over_ranks(elapsed, dist, device=red_dev)
-    iso_ms = None
-    if use_events and S > 1:  # reference: the same launches one at a time on one stream (untimed for `value`)
+    if use_events and S > 1 and not iso_first:  # reference: the same launches one at a time on one stream (untimed for `value`)
         _, iso_ms = timed(max(args.steps, 20), args.warmup + args.steps, 1)
 
     total_bytes = bytes_per_step * args.steps * world  # every rank processed bytes_per_step per step
