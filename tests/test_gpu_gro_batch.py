@@ -181,3 +181,68 @@ def test_gro_batch_host_test_scenarios(dev):
         (big, 65535, True, None),
     ] + [(inv, 65535, True, {bad_at: OFFSET}) for bad_at in (1, 5, 9, 13)]
     assert _check(dev, calls) == len(calls)
+
+
+def _tcp_pkt(src, dst, sport, dport, seq, flags, opts, payload, v6):
+    """One TCP segment with options and valid IPv4 / TCP checksums (oracle
+    checksum functions: test infrastructure)."""
+    import struct
+
+    th = 20 + len(opts)
+    tcp = bytearray(struct.pack("!HHIIBBHHH", sport, dport, seq & 0xFFFFFFFF, 7, (th // 4) << 4, flags, 65535, 0, 0)
+                    + opts + payload)
+    if v6:
+        ip = bytearray(struct.pack("!IHBB", 0x60000000, len(tcp), 6, 64) + src + dst)
+    else:
+        ip = bytearray(struct.pack("!BBHHHBBH4s4s", 0x45, 0, 20 + len(tcp), 0x1234, 0x4000, 64, 6, 0, src, dst))
+        ip[10:12] = ((~oracle.checksum(bytes(ip), 0)) & 0xFFFF).to_bytes(2, "big")
+    c = (~oracle.checksum(bytes(tcp), oracle.pseudo_header_nofold(src, dst, 6, len(tcp)))) & 0xFFFF
+    tcp[16:18] = c.to_bytes(2, "big")
+    return bytes(ip + tcp)
+
+
+def _opt_flow(rng, nseg, mss, v6, same_opts, seed):
+    src = bytes(rng.integers(0, 256, 16 if v6 else 4, dtype=np.uint8))
+    dst = bytes(rng.integers(0, 256, 16 if v6 else 4, dtype=np.uint8))
+    sport, dport = 1000 + seed, 51820
+    seq0 = int(rng.integers(0, 2**32))
+    out = []
+    for k in range(nseg):
+        ts = 1000 if same_opts else 1000 + k
+        opts = bytes([1, 1, 8, 10]) + ts.to_bytes(4, "big") + (99).to_bytes(4, "big")  # NOP NOP TS
+        flags = 0x18 if k == nseg - 1 and rng.random() < 0.5 else 0x10
+        out.append(_tcp_pkt(src, dst, sport, dport, seq0 + k * mss, flags, opts,
+                            bytes(rng.integers(0, 256, mss, dtype=np.uint8)), v6))
+    return out
+
+
+def test_gro_batch_tcp_options_fuzz(dev):
+    """Random Write calls mixing TCP flows with timestamp options (equal
+    options coalesce, changing ones do not: gro.go:442-448), flows without
+    options, UDP, reordering (prepends), tight capacities and corrupted
+    checksums -- the register fast path falls back to the LDS path for every
+    one of these."""
+    rng = np.random.default_rng(2024)
+    calls = []
+    for k in range(40):
+        flows = []
+        for j in range(int(rng.integers(1, 6))):
+            kind = int(rng.integers(0, 4))
+            n = int(rng.integers(1, 20))
+            mss = int(rng.choice([536, 1000, 1448]))
+            if kind == 0:
+                flows.append(_opt_flow(rng, n, mss, bool(rng.integers(0, 2)), True, 10 * k + j))
+            elif kind == 1:
+                flows.append(_opt_flow(rng, n, mss, bool(rng.integers(0, 2)), False, 10 * k + j))
+            else:
+                flows.append(flow(n, seg=mss, v6=bool(rng.integers(0, 2)), udp=kind == 3, seed=5000 + 10 * k + j,
+                                  last_flags=int(rng.choice([0x10, 0x18]))))
+        pk = [p for f in flows for p in f][:128]
+        noise = rng.random(len(pk)) * (3.0 if k % 3 == 0 else 0.3)  # sometimes heavy reordering
+        pk = [pk[i] for i in np.argsort(np.arange(len(pk)) * 0.1 + noise)]
+        for _ in range(int(rng.integers(0, 3))):
+            i = int(rng.integers(0, len(pk)))
+            b = bytearray(pk[i]); b[-1] ^= 0x24; pk[i] = bytes(b)
+        cap = 65535 if k % 4 else (lambda n, e=int(rng.integers(0, 4000)): OFFSET + n + e)
+        calls.append((pk, cap, bool(k % 5), None))
+    assert _check(dev, calls) == len(calls)
