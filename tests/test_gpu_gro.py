@@ -154,3 +154,17 @@ def test_batch_size_128(dev):
     perm = rng.permutation(len(pkts))
     run_both(dev, [pkts[i] for i in perm])
     run_both(dev, pkts)
+
+
+def test_tcp_options_host_path(dev):
+    """wgcs_handle_gro (host planner) on flows with TCP timestamp options:
+    equal options coalesce, changing ones do not (gro.go:442-448)."""
+    from test_gpu_gro_batch import _opt_flow
+
+    rng = np.random.default_rng(77)
+    for k in range(6):
+        fa = _opt_flow(rng, 7, 1000, bool(k & 1), True, 2 * k)
+        fb = _opt_flow(rng, 5, 1448, bool(k & 2), False, 2 * k + 1)
+        pk = fa + fb + flow(4, seed=300 + k)
+        order = np.argsort(rng.random(len(pk)) * (2.0 if k > 2 else 0.2) + np.arange(len(pk)) * 0.1)
+        run_both(dev, [pk[i] for i in order])
