@@ -1,6 +1,8 @@
 """GPU parity: GSO split (handleVirtioRead / gsoSplit, tun/tun.go:514-632 +
 tun/gro.go:1373-1517) vs the oracle -- every output byte, size, count, error
 code and the reference's readBuf mutations, through the C ABI."""
+import struct
+
 import numpy as np
 import pytest
 
@@ -351,3 +353,25 @@ def test_device_batch_cfg4_like(dev):
         assert list(sizes[j, :w]) == sz_o[:w]
         for i in range(max_segs):
             assert np.array_equal(out[j, i], bo[i]), (j, i)
+
+
+@pytest.mark.parametrize("v6,udp", [(False, False), (True, False), (False, True)])
+@pytest.mark.parametrize("total,gso", [(65535, 1460), (1500, 1460), (1460, 1460)])
+def test_empty_bufs_split(dev, v6, udp, total, gso):
+    """len(bufs) == 0: gsoSplit's loop returns (-1, ErrTooManySegments)
+    before touching bufs (gro.go:1408-1410) after readBuf was prepared, or
+    (0, nil) when the read holds no segment; validation errors come first."""
+    vp = synth.make_super_packet(total, gso, seed=41, v6=v6, udp=udp)
+    o, p = run_both(dev, vp, nbufs=0)
+    assert_same(o, p)
+    # the raw gsoSplit entry point, same header
+    h = tuple(int(x) for x in struct.unpack("<BBHHHH", vp[:10]))
+    o, p = run_both_raw(dev, vp[10:], h, v6, nbufs=0)
+    assert_same(o, p)
+
+
+def test_empty_bufs_gso_none(dev):
+    """GSO_NONE with len(bufs) == 0 indexes bufs[0]: a Go panic, OUT_OF_RANGE."""
+    pkt = synth.make_super_packet(1500, 1460, seed=42)[10:]
+    n, err = dev.handle_virtio_read(bytes(10) + pkt, [], [], 16)
+    assert err is not None and err.code == -13 and n == 0

@@ -37,13 +37,21 @@ struct GsoResult {
 // code would panic on the slice.  Caller holds ctx->mu.
 int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflags, uint8_t* const* bufs,
                  const size_t* buf_lens, int nbufs, int* sizes, int offset, GsoResult* res) {
-  if (nbufs <= 0 || !bufs || !buf_lens || !sizes || offset < 0)
+  if (nbufs < 0 || (nbufs > 0 && (!bufs || !buf_lens || !sizes)) || offset < 0)
     return set_err(ctx, WGCS_ERR_INVALID_ARG, "bufs/sizes/offset");
   if (vlen > 0x7FFFFFF0u) return set_err(ctx, WGCS_ERR_INVALID_ARG, "super-packet too large");
-  if (buf_lens[0] < (size_t)offset) return set_err(ctx, WGCS_ERR_OUT_OF_RANGE, "offset beyond bufs[0]");
-  const size_t room = std::min<size_t>(buf_lens[0] - (size_t)offset, 0xFFFFFFFFu);
+  // len(bufs) == 0: the reference validates and prepares readBuf exactly as
+  // usual, then fails at the first bufs access -- gsoSplit's loop returns
+  // (i-1 = -1, ErrTooManySegments) before touching bufs[0] (gro.go:1408-1410),
+  // handleVirtioRead's GSO_NONE path indexes bufs[0] (a panic: OUT_OF_RANGE),
+  // and a split that yields no segment returns (0, nil).  The kernel runs the
+  // job against one scratch slot of unbounded room to get that verdict.
+  const bool nobuf = nbufs == 0;
+  const int kbufs = nobuf ? 1 : nbufs;
+  if (!nobuf && buf_lens[0] < (size_t)offset) return set_err(ctx, WGCS_ERR_OUT_OF_RANGE, "offset beyond bufs[0]");
+  const size_t room = nobuf ? 0xFFFFFFFFu : std::min<size_t>(buf_lens[0] - (size_t)offset, 0xFFFFFFFFu);
   uint32_t pitch, nseg_bound;
-  gso_out_layout(vbuf, vlen, jflags, (uint32_t)nbufs, &pitch, &nseg_bound);
+  gso_out_layout(vbuf, vlen, jflags, (uint32_t)kbufs, &pitch, &nseg_bound);
   if (pitch == 0) pitch = 16;
   const size_t region = (size_t)pitch * nseg_bound;
   // header geometry as the kernel will see it (for the per-buffer slice checks)
@@ -54,10 +62,10 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   const bool v4 = raw ? (jflags & WGCS_GSO_JOB_V6) == 0 : (vlen > 10 && (vbuf[10] >> 4) == 4);
   // An IPv4 header shorter than 6 bytes makes the id update read bufs[i]'s own
   // bytes 4-5 (gro.go:1427): the kernel reads them from the segment's slot.
-  const bool stale_id = (raw || gtype != 0) && v4 && cs <= 5 && region;
+  const bool stale_id = (raw || gtype != 0) && v4 && cs <= 5 && region && !nobuf;
   hipSetDevice(ctx->device);
   int rc;
-  const size_t meta = ((size_t)nbufs * 4 + 16 + 15) & ~(size_t)15;  // sizes[nbufs] | count | status
+  const size_t meta = ((size_t)kbufs * 4 + 16 + 15) & ~(size_t)15;  // sizes[kbufs] | count | status
   const size_t aux = sizeof(wgcs_gso_job) + sizeof(GsoOutPos);
   if ((rc = ensure_pinned(ctx, ctx->h_meta, meta + aux)) || (rc = ensure_pinned(ctx, ctx->h_stage, region + 16)))
     return rc;
@@ -80,12 +88,25 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   }
   // pinned staging is mapped into the device's address space at its host
   // address (checked by ensure_pinned's hipHostMalloc contract, see api.cpp)
-  hipError_t e = launch_gso_split_batch(vbuf, hjob, 1, hs, 0, 0, (uint32_t)nbufs, h, h + nbufs, h + nbufs + 1, s,
+  hipError_t e = launch_gso_split_batch(vbuf, hjob, 1, hs, 0, 0, (uint32_t)kbufs, h, h + kbufs, h + kbufs + 1, s,
                                         hpos, (uint32_t)room);
   if (e != hipSuccess) return hip_fail(ctx, e, "gso_split launch");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "gso_split wait");
-  res->count = h[nbufs];
-  res->status = h[nbufs + 1];
+  res->count = h[kbufs];
+  res->status = h[kbufs + 1];
+  if (nobuf) {
+    const bool none = !raw && gtype == 0;  // handleVirtioRead's GSO_NONE path
+    if (res->status == 0 && none) {
+      res->status = WGCS_ERR_OUT_OF_RANGE;  // bufs[0] of an empty bufs
+      res->count = 0;
+    } else if ((res->status == 0 && res->count > 0) || res->status == WGCS_ERR_TOO_MANY_SEGMENTS) {
+      res->status = WGCS_ERR_TOO_MANY_SEGMENTS;
+      res->count = -1;
+    } else if (res->status != 0) {
+      res->count = 0;
+    }
+    return WGCS_OK;
+  }
   if (res->status != 0 && res->status != WGCS_ERR_TOO_MANY_SEGMENTS) {
     res->count = 0;
     return WGCS_OK;
