@@ -297,7 +297,7 @@ def cpu_baseline(pkts, seconds):
                           "sample": f"{calls_mt} calls on {threads} pthreads, each on a private copy of the batch"}}
 
 
-def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int = 1280, rotate: int = 4):
+def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int = 1792, rotate: int = 4):
     """bench.py --config gro_device: the device-resident batch of Tun.Write
     calls (wgcs_handle_gro_batch).  One step = one launch over `calls` calls
     of the 128-packet batch above, every buffer a Go-sized slice (cap 65,551 B)
