@@ -547,36 +547,64 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
   if (t < n_eff) {
     const uint8_t* pk = arena + S.boff[t] + offset;
     const uint32_t pl = S.blen[t] - (uint32_t)offset;
+    // Every field below lies in the first 64 packet bytes (IPv4 with IHL 5
+    // or IPv6, then the TCP / UDP header).  A packet of >= 80 bytes brings
+    // them in with one batch of five aligned 16-byte loads (all inside the
+    // packet), shifted to packet coordinates: one memory round trip instead
+    // of a chain of dependent byte loads.  A shorter one reads byte by byte.
+    const bool win = pl >= 80;
+    uint4 P0 = make_uint4(0, 0, 0, 0), P1 = P0, P2 = P0, P3 = P0;
+    if (win) {
+      const uint8_t* a0 = reinterpret_cast<const uint8_t*>((uintptr_t)pk & ~(uintptr_t)15);
+      const int sh = (int)((uintptr_t)pk & 15u);
+      const uint4 c0 = ld16(a0), c1 = ld16(a0 + 16), c2 = ld16(a0 + 32), c3 = ld16(a0 + 48), c4 = ld16(a0 + 64);
+      P0 = funnel(c0, c1, sh);
+      P1 = funnel(c1, c2, sh);
+      P2 = funnel(c2, c3, sh);
+      P3 = funnel(c3, c4, sh);
+    }
+    // byte k (< 64, a compile-time constant after unrolling) of the packet
+    auto B = [&](int k) -> uint32_t {
+      if (!win) return pk[k];
+      const uint4& q = k < 16 ? P0 : (k < 32 ? P1 : (k < 48 ? P2 : P3));
+      const int d = (k >> 2) & 3;
+      const uint32_t w = d == 0 ? q.x : (d == 1 ? q.y : (d == 2 ? q.z : q.w));
+      return (w >> (8 * (k & 3))) & 0xFFu;
+    };
+    auto BE16 = [&](int k) -> uint32_t { return (B(k) << 8) | B(k + 1); };
+    auto BE32 = [&](int k) -> uint32_t { return (BE16(k) << 16) | BE16(k + 2); };
     uint8_t c = C_NOT;
     if (pl >= 28) {  // gro.go:1280-1317
-      const uint32_t v = pk[0] >> 4;
-      if (v == 4 && (pk[0] & 0x0F) == 5) {
-        if (pk[9] == 6 && pl >= 40) c = C_TCP4;
-        else if (pk[9] == 17 && can_udp) c = C_UDP4;
+      const uint32_t b0 = B(0), v = b0 >> 4;
+      if (v == 4 && (b0 & 0x0F) == 5) {
+        const uint32_t pr = B(9);
+        if (pr == 6 && pl >= 40) c = C_TCP4;
+        else if (pr == 17 && can_udp) c = C_UDP4;
       } else if (v == 6) {
-        if (pk[6] == 6 && pl >= 60) c = C_TCP6;
-        else if (pk[6] == 17 && pl >= 48 && can_udp) c = C_UDP6;
+        const uint32_t nh = B(6);
+        if (nh == 6 && pl >= 60) c = C_TCP6;
+        else if (nh == 17 && pl >= 48 && can_udp) c = C_UDP6;
       }
     }
     S.cand[t] = c;
     if (c != C_NOT) {
       const bool v6 = c == C_TCP6 || c == C_UDP6, tcp = c <= C_TCP6;
-      const int ih = v6 ? 40 : (pk[0] & 0x0F) * 4;
+      const int ih = v6 ? 40 : 20;  // IPv4 candidates have IHL 5
       bool nop = pl > 65535;
-      if (v6) nop = nop || be16g(pk + 4) != pl - 40;
-      else nop = nop || be16g(pk + 2) != pl;
+      if (v6) nop = nop || BE16(4) != pl - 40;
+      else nop = nop || BE16(2) != pl;
       int thl = 8;
       uint32_t fl = 0;
       if (tcp) {
         nop = nop || pl < (uint32_t)ih;
-        thl = (pk[ih + 12] >> 4) * 4;
+        thl = (int)((v6 ? B(52) : B(32)) >> 4) * 4;
         nop = nop || thl < 20 || thl > 60 || pl < (uint32_t)(ih + thl);
       } else {
         nop = nop || pl < (uint32_t)(ih + 8);
       }
-      if (!v6) nop = nop || (pk[6] & 0x20) || (uint8_t)(pk[6] << 3) || pk[7];  // fragments
+      if (!v6) nop = nop || (B(6) & 0x20) || (uint8_t)(B(6) << 3) || B(7);  // fragments
       if (!nop && tcp) {
-        fl = pk[ih + 13];
+        fl = v6 ? B(53) : B(33);
         nop = fl != 0x10 && fl != 0x18;  // ACK, or ACK|PSH
       }
       const int g = nop ? 0 : (int)pl - ih - thl;
@@ -587,25 +615,29 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
       S.psh[t] = (fl & 0x08) ? 1 : 0;
       S.gso[t] = (uint16_t)g;
       if (!nop) {
-        S.seq[t] = tcp ? be32g(pk + ih + 4) : 0u;
-        S.ipattr[t] = v6 ? (uint32_t)pk[0] | ((uint32_t)(pk[1] >> 4) << 8) | ((uint32_t)pk[7] << 16) | (6u << 24)
-                         : (uint32_t)pk[1] | ((uint32_t)(pk[6] >> 5) << 8) | ((uint32_t)pk[8] << 16) | (4u << 24);
-        // flow key words (addresses, ports, ack for TCP) into LDS + their hash;
-        // the byte loads are independent (fixed trip counts)
-        const int a_lo = v6 ? 8 : 12, nab = v6 ? 32 : 8;
+        S.seq[t] = tcp ? (v6 ? BE32(44) : BE32(24)) : 0u;
+        S.ipattr[t] = v6 ? B(0) | ((B(1) >> 4) << 8) | (B(7) << 16) | (6u << 24)
+                         : B(1) | ((B(6) >> 5) << 8) | (B(8) << 16) | (4u << 24);
+        // flow key words (addresses, ports, ack for TCP) into LDS + their hash
         uint32_t h = 2166136261u;
+        if (v6) {
 #pragma unroll
-        for (int w = 0; w < 8; ++w) {
-          uint32_t x = 0;
-          if (4 * w < nab)
+          for (int w = 0; w < 8; ++w) {
+            const uint32_t x = BE32(8 + 4 * w);
+            S.kw[t][w] = x;
+            h = fnv(h, x);
+          }
+        } else {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) x = (x << 8) | pk[a_lo + 4 * w + k];
-          if (4 * w < nab) {
+          for (int w = 0; w < 2; ++w) {
+            const uint32_t x = BE32(12 + 4 * w);
             S.kw[t][w] = x;
             h = fnv(h, x);
           }
         }
-        const uint32_t ports = be32g(pk + ih), ack = tcp ? be32g(pk + ih + 8) : 0u;
+        const int nab = v6 ? 32 : 8;
+        const uint32_t ports = v6 ? BE32(40) : BE32(20);
+        const uint32_t ack = tcp ? (v6 ? BE32(48) : BE32(28)) : 0u;
         S.kw[t][nab / 4] = ports;
         S.kw[t][nab / 4 + 1] = ack;
         S.keyh[t] = fnv(fnv(fnv(h, ports), ack), c);
