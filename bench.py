@@ -73,8 +73,48 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launcher_cmd(gpus: int, argv: list[str], port: int) -> list[str]:
+    """The torch.distributed.run command that runs this bench as `gpus` ranks
+    (one process per GPU) with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(args, argv: list[str]) -> int | None:
+    """`--gpus N` without a launcher: run N ranks under torch.distributed.run as
+    a CHILD process (started before torch or HIP is touched in this process;
+    never exec) and return its exit code.  Under a launcher, WORLD_SIZE must
+    equal --gpus.  Returns None when this process is itself the (only) rank."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import subprocess
+
+    return subprocess.run(launcher_cmd(args.gpus, argv, _free_port())).returncode
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    rc = launch_ranks(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     if args.streams <= 0:
         args.streams = 1 if args.config in ("cfg1", "cfg5") else 2
     import torch  # before wireguard_amd: one HIP runtime per process
@@ -91,6 +131,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
+        if backend == "nccl" and torch.cuda.device_count() < world:
+            sys.exit(f"bench.py: {world} RCCL ranks need {world} GPUs, {torch.cuda.device_count()} visible "
+                     "(WGCS_DIST_BACKEND=gloo rehearses ranks sharing a GPU)")
         local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -148,34 +191,31 @@ def main():
     outs = [torch.empty(n * 2, dtype=torch.uint8, device="cuda") for _ in range(R)]
     torch.cuda.synchronize()
 
-    def step(k, ns=S):
-        i = k % R
-        dev.checksum_batch(mode, arenas[i], pkts, n, outs[i], stream=streams[k % ns])
+    def batches(K, k0):  # steps k0 .. k0+K-1: each its own rotated arena and output
+        return dev.batch_list([(arenas[(k0 + k) % R], pkts, n, outs[(k0 + k) % R]) for k in range(K)])
 
-    # HIP events bracket the timed region on the launch streams: e0 on stream 0
-    # (the others wait on it), every other stream joins stream 0 before e1, so
-    # (e1 - e0) / steps is the GPU time per launch over the timed region (an
-    # event between launches would add a gap per step).
+    def step(k, ns=S):
+        dev.checksum_batches(mode, batches(1, k), streams[k % ns: k % ns + 1])
+
+    # The K steps are enqueued by ONE library call (wgcs_checksum_batches: step k
+    # on stream k % S), which also records the HIP bracket events on the launch
+    # streams: e0 on stream 0 before the first launch (the others wait on it),
+    # every other stream joined to stream 0 before e1, so (e1 - e0) / K is the
+    # GPU time per launch over the timed region.  One call instead of K Python
+    # calls: the first launch leaves the host ~10 us sooner and no per-step
+    # ctypes/torch path runs inside the region.
     use_events = not args.no_event_timing
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
-    joins = [torch.cuda.Event() for _ in streams[1:]]
+    e0.record(streams[0])  # torch creates the HIP events on their first record
+    e1.record(streams[0])
 
     def timed(K, k0, ns):
+        bl = batches(K, k0)  # the step list (pointers only) is built before the clock starts
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        if use_events:
-            e0.record(streams[0])
-            for st in streams[1:ns]:
-                st.wait_event(e0)
-        for k in range(K):
-            step(k0 + k, ns)
-        for j, st in zip(joins, streams[1:ns]):
-            j.record(st)
-            streams[0].wait_event(j)
-        if use_events:
-            e1.record(streams[0])
+        dev.checksum_batches(mode, bl, streams[:ns], e0 if use_events else None, e1 if use_events else None)
         torch.cuda.synchronize()
         barrier()
         el = time.perf_counter() - t0
@@ -205,8 +245,8 @@ def main():
             want = (a[np.arange(n), cs].astype(np.uint16) << 8) | a[np.arange(n), cs + 1]
             assert np.array_equal(got, want), "L4_FILL mismatch vs stored checksums"
 
-    elapsed, kern_ms = timed(args.steps, args.warmup, S)
-    elapsed = shard.max_over_ranks(elapsed, dist, device=red_dev)
+    local_elapsed, kern_ms = timed(args.steps, args.warmup, S)
+    elapsed = shard.max_over_ranks(local_elapsed, dist, device=red_dev)
     if use_events and S > 1 and not iso_first:  # reference: the same launches one at a time on one stream (untimed for `value`)
         _, iso_ms = timed(max(args.steps, 20), args.warmup + args.steps, 1)
 
@@ -245,6 +285,11 @@ def main():
         },
     }
     if kern_ms is not None:
+        # host-side time inside the timed region beyond the GPU's event span:
+        # first-launch latency + the completion wait (this rank; `value` uses the max over ranks)
+        result["timing"] = {"wall_us": round(local_elapsed * 1e6, 2), "event_span_us": round(kern_ms * args.steps * 1e3, 2),
+                            "wall_minus_span_us": round((local_elapsed - kern_ms * args.steps * 1e-3) * 1e6, 2),
+                            "enqueue": "one wgcs_checksum_batches call for the K steps"}
         achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
         result["roofline"] = {
             "bound": "hbm",

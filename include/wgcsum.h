@@ -155,6 +155,28 @@ int wgcs_checksum_batch(wgcs_ctx *ctx, int mode, unsigned flags, uint8_t *d_aren
                         const wgcs_pkt *d_pkts, const uint64_t *d_initial, uint32_t n,
                         void *d_out, void *stream);
 
+/* A series of independent device-resident batches enqueued by one call (e.g.
+ * consecutive Tun.Read/Write batches, tun/tun.go:477-508, :654-700, already in
+ * HBM): batch k is launched on streams[k % n_streams] (n_streams 0: the
+ * context's stream), in order, with wgcs_checksum_batch's semantics.  Optional
+ * bracket events (hipEvent_t as void*, created by the caller): ev_begin is
+ * recorded on streams[0] before the first launch and the other streams wait on
+ * it before their first; after the last launch every other stream is joined
+ * to streams[0] and ev_end is recorded there, so the pair spans every launch.
+ * All arguments are checked before anything is enqueued. */
+typedef struct wgcs_batch {
+  uint8_t *arena;
+  const wgcs_pkt *pkts;
+  const uint64_t *initial; /* FOLD only; may be NULL */
+  void *out;
+  uint32_t n;
+  uint32_t pad;
+} wgcs_batch;
+#define WGCS_MAX_BATCH_STREAMS 16
+int wgcs_checksum_batches(wgcs_ctx *ctx, int mode, unsigned flags, const wgcs_batch *batches,
+                          uint32_t n_batches, void *const *streams, uint32_t n_streams,
+                          void *ev_begin, void *ev_end);
+
 /* gsoSplit for n_jobs super-packets.  Job j writes its segments into output
  * slots [j*max_segs, (j+1)*max_segs), slot s at d_out + s*out_stride + offset
  * (like bufs[s][offset:]).  d_sizes[slot] = packet size; d_count[j] = the

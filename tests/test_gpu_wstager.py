@@ -259,3 +259,95 @@ def test_write_stager_pinned_rejects_pageable(dev):
         ws.push_pinned(bufs, lens, OFFSET, True)
     assert getattr(ei.value, "code", None) == -1, ei.value
     ws.close()
+
+
+def test_write_stager_concurrent_submits(dev):
+    """Four pushing threads and two submitting threads at once (a
+    submit that waited for copying pushes must not queue a stale slot): every
+    submit returns a distinct batch, and the calls found in the submitted
+    batches are exactly the pushed calls, each with its own handleGRO result."""
+    import threading
+
+    calls = _calls(8)[:16]
+    ws = WriteStager(dev, depth=16, max_writes=4, max_pkts=4 * 128, max_bytes=4 * 128 * 1600)
+    lock = threading.Lock()
+    batches, keep = [], []
+    stop = threading.Event()
+
+    def submit():
+        b = ws.submit()
+        with lock:
+            batches.append(b)
+
+    def pusher(t):
+        for k in range(t, len(calls), 4):
+            pkts, cap, can_udp, lo = calls[k]
+            bufs, lens = _mk(pkts, cap, OFFSET, lo)
+            with lock:
+                keep.append(bufs)
+            while True:
+                try:
+                    ws.push(bufs, lens, OFFSET, can_udp)
+                    break
+                except Exception as e:  # BATCH_FULL: submit the open slot and push again
+                    assert getattr(e, "code", None) == -14, e
+                    submit()
+
+    def submitter():
+        for _ in range(3):
+            if stop.wait(0.002):
+                break
+            submit()
+
+    th = [threading.Thread(target=pusher, args=(t,)) for t in range(4)] + \
+         [threading.Thread(target=submitter) for _ in range(2)]
+    for x in th:
+        x.start()
+    for x in th[:4]:
+        x.join()
+    stop.set()
+    for x in th[4:]:
+        x.join()
+    submit()
+    assert len(batches) < 16, "results would have been recycled"
+    assert len(set(batches)) == len(batches), f"a slot was submitted twice: {batches}"
+    want = {}
+    for k, (pkts, cap, can_udp, lo) in enumerate(calls):
+        rc, tw, writes = _oracle_writes(pkts, cap, can_udp, OFFSET, lo)
+        want[k] = (rc, tw, writes)
+    found = []
+    for b in batches:
+        ws.wait(b)
+        idx = 0
+        while True:
+            try:
+                err, tw_p, writes_p = ws.result(b, idx, 128)
+            except Exception as e:
+                assert getattr(e, "code", None) == -1, e  # past the slot's last call
+                break
+            found.append((0 if err is None else err.code, tw_p, writes_p))
+            idx += 1
+    assert len(found) == len(calls)
+    for k, w in want.items():  # the seeded flows make every call's writes distinct
+        assert found.count(w) >= 1, f"call {k} missing from the submitted batches"
+    ws.close()
+
+
+def test_host_free_refused_while_a_slot_reads_it(dev):
+    """wgcs_host_free refuses (NOT_READY) pinned memory that an open write-stager
+    slot still reads through a zero-copy push; after the slot ran it succeeds."""
+    pkts = flow(6, seed=11)
+    pool = dev.host_alloc(8 * 65536)
+    ws = WriteStager(dev, depth=2, max_writes=4, max_pkts=512, max_bytes=512 * 1600)
+    bufs, lens, _ = _mk_pinned(pool, 0, pkts, 65535, OFFSET, None, lambda i: 0)
+    idx = ws.push_pinned(bufs, lens, OFFSET, True)
+    with pytest.raises(Exception) as ei:
+        dev.host_free(pool)
+    assert getattr(ei.value, "code", None) == -15, ei.value
+    b = ws.submit()
+    ws.wait(b)
+    rc, tw, writes = _oracle_writes(pkts, 65535, True, OFFSET, None)
+    err, tw_p, writes_p = ws.result(b, idx, len(pkts))
+    assert (0 if err is None else err.code, tw_p, writes_p) == (rc, tw, writes)
+    dev.host_free(pool)
+    ws.close()

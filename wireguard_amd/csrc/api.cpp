@@ -167,6 +167,9 @@ int wgcs_host_free(wgcs_ctx* ctx, void* p) {
       return r.first == (uintptr_t)p;
     });
     if (it == v.end()) return set_err(ctx, WGCS_ERR_INVALID_ARG, "wgcs_host_free: not a wgcs_host_alloc pointer");
+    for (wgcs_wstager* ws : ctx->wstagers)
+      if (wstager_references(ws, it->first, it->second))
+        return set_err(ctx, WGCS_ERR_NOT_READY, "wgcs_host_free: a write-stager slot still reads this memory");
     v.erase(it);
   }
   const hipError_t e = hipHostFree(p);
@@ -175,6 +178,12 @@ int wgcs_host_free(wgcs_ctx* ctx, void* p) {
 
 int wgcs_destroy(wgcs_ctx* ctx) {
   if (!ctx) return WGCS_ERR_INVALID_ARG;
+  {
+    std::lock_guard<std::mutex> g(ctx->host_mu);
+    if (!ctx->wstagers.empty())  // their slots use the context and may read its host allocations
+      return set_err(ctx, WGCS_ERR_INVALID_ARG, "wgcs_destroy: %zu write stager(s) still alive: destroy them first",
+                     ctx->wstagers.size());
+  }
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
   for (const auto& r : ctx->host_allocs) hipHostFree((void*)r.first);
@@ -183,6 +192,8 @@ int wgcs_destroy(wgcs_ctx* ctx) {
   for (HostBuf* b : {&ctx->h_stage, &ctx->h_meta, &ctx->h_out})
     if (b->ptr) hipHostFree(b->ptr);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
+  for (hipEvent_t ev : ctx->join_ev)
+    if (ev) hipEventDestroy(ev);
   delete ctx;
   return WGCS_OK;
 }
@@ -237,6 +248,49 @@ int wgcs_checksum_batch(wgcs_ctx* ctx, int mode, unsigned flags, uint8_t* d_aren
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   hipError_t e = launch_checksum_batch(mode, flags, d_arena, d_pkts, d_initial, n, d_out, s, ctx->num_cu, ctx->tune);
   return e == hipSuccess ? WGCS_OK : hip_fail(ctx, e, "checksum_batch launch");
+}
+
+int wgcs_checksum_batches(wgcs_ctx* ctx, int mode, unsigned flags, const wgcs_batch* batches, uint32_t n_batches,
+                          void* const* streams, uint32_t n_streams, void* ev_begin, void* ev_end) {
+  if (!ctx) return WGCS_ERR_INVALID_ARG;
+  if (mode < WGCS_MODE_FOLD || mode > WGCS_MODE_IP4HDR) return set_err(ctx, WGCS_ERR_INVALID_ARG, "bad mode %d", mode);
+  if (n_streams > WGCS_MAX_BATCH_STREAMS || (n_streams && !streams) || (n_batches && !batches))
+    return set_err(ctx, WGCS_ERR_INVALID_ARG, "bad stream list (%u streams)", n_streams);
+  for (uint32_t k = 0; k < n_batches; ++k)
+    if (batches[k].n && (!batches[k].arena || !batches[k].pkts || !batches[k].out))
+      return set_err(ctx, WGCS_ERR_INVALID_ARG, "batch %u: NULL pointer", k);
+  std::lock_guard<std::mutex> g(ctx->mu);
+  hipSetDevice(ctx->device);
+  const uint32_t ns = n_streams ? n_streams : 1;
+  hipStream_t st[WGCS_MAX_BATCH_STREAMS];
+  for (uint32_t j = 0; j < ns; ++j) st[j] = n_streams && streams[j] ? (hipStream_t)streams[j] : ctx->stream;
+  hipError_t e = hipSuccess;
+  if (ev_end)
+    for (uint32_t j = 1; j < ns && e == hipSuccess; ++j)
+      if (!ctx->join_ev[j]) e = hipEventCreateWithFlags(&ctx->join_ev[j], hipEventDisableTiming);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipEventCreate");
+  // ev_begin, then batch 0 at once (the first launch is the latency-critical
+  // one); each other stream waits on ev_begin just before its first launch
+  if (ev_begin && (e = hipEventRecord((hipEvent_t)ev_begin, st[0])) != hipSuccess) return hip_fail(ctx, e, "ev_begin");
+  for (uint32_t k = 0; k < n_batches; ++k) {
+    const uint32_t j = k % ns;
+    if (ev_begin && j != 0 && k < ns && st[j] != st[0] &&
+        (e = hipStreamWaitEvent(st[j], (hipEvent_t)ev_begin, 0)) != hipSuccess)
+      return hip_fail(ctx, e, "stream wait");
+    const wgcs_batch& b = batches[k];
+    e = launch_checksum_batch(mode, flags, b.arena, b.pkts, b.initial, b.n, b.out, st[j], ctx->num_cu, ctx->tune);
+    if (e != hipSuccess) return hip_fail(ctx, e, "checksum_batches launch");
+  }
+  if (ev_end) {
+    for (uint32_t j = 1; j < ns; ++j) {
+      if (st[j] == st[0]) continue;
+      if ((e = hipEventRecord(ctx->join_ev[j], st[j])) != hipSuccess ||
+          (e = hipStreamWaitEvent(st[0], ctx->join_ev[j], 0)) != hipSuccess)
+        return hip_fail(ctx, e, "stream join");
+    }
+    if ((e = hipEventRecord((hipEvent_t)ev_end, st[0])) != hipSuccess) return hip_fail(ctx, e, "ev_end");
+  }
+  return WGCS_OK;
 }
 
 // Host batches up to this size run zero-copy (the kernel reads pinned staging

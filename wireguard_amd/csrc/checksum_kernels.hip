@@ -7,14 +7,21 @@
 //   gsoNoneChecksum()              /root/reference/tun/gro.go:1497-1517
 //   IPv4 header checksum sites     /root/reference/tun/gro.go:1134-1138,1434-1436
 //
-// Design: one wave64 per packet, persistent grid-stride
-// over packets.  Each lane streams 16-byte aligned chunks of the packet with
-// global_load_dwordx4 (1 KiB per wave instruction, U instructions in flight
-// per lane), masks head/tail/excluded bytes, and accumulates little-endian
-// u32 words into a u64.  Per-lane fold to 16 bits, DPP wave sum, parity
-// correction, pseudo-header / initial, final fold.  No LDS: each byte is read
-// once and used once (HBM-streaming reduction, cdna_hip_programming.md
-// "GEMV / M <= 16" row), no MFMA (byte reduction, not a contraction).
+// Design: the launched kernel is checksum_batch_kernel<MODE,
+// G = 32, U = 4, NT>: one G-lane group (half a wave64) per packet, two packets
+// per wave, persistent grid-stride over packets with an XCD-aware block order.
+// Each lane streams 16-byte chunks of its packet with non-temporal
+// global_load_dwordx4 (U loads in flight per lane: 2 KiB per half-wave step,
+// so one iteration covers a 1500-B frame), masks only the head / checksum
+// field / tail chunks, and adds both u16 halves of every dword into a u32
+// accumulator with one v_dot2 (re-folded each iteration).  Per-lane fold to 16
+// bits, DPP row sums + one cross-row exchange, parity correction,
+// pseudo-header / initial, final fold.  G = 16 (a DPP row) and G = 64 (a
+// wave) are the tuning alternatives (WGCS_LANES_PER_PKT).  No LDS staging:
+// each byte is read once and used once, and a 16-B register load per lane
+// already moves 1 KiB per wave instruction -- measured, LDS-DMA staging ties
+// register loads on this pattern (profiles/r1_probe_glds.jsonl) -- and no MFMA
+// (a byte reduction, not a contraction).
 #include <hip/hip_runtime.h>
 
 #include "../../include/wgcsum.h"

@@ -69,6 +69,7 @@ struct wgcs_stager {
   std::vector<Slot> slots;
   uint32_t open = 0;
   uint64_t next_id = 1;
+  bool broken = false;  // a ring slot could not be opened (HIP error): every later call fails
   std::mutex mu;
 
   size_t meta_words() const { return (size_t)max_reads * max_segs + 2 * (size_t)max_reads; }
@@ -102,7 +103,10 @@ int open_slot(wgcs_stager* st, uint32_t idx) {
   Slot& s = st->slots[idx];
   if (s.state == 2) {
     hipError_t e = hipEventSynchronize(s.done);
-    if (e != hipSuccess) return hip_fail(st->ctx, e, "stager: wait for ring slot");
+    if (e != hipSuccess) {
+      st->broken = true;  // st->open still names the submitted slot: nothing may be staged into it
+      return hip_fail(st->ctx, e, "stager: wait for ring slot (stager unusable)");
+    }
   }
   s.id = st->next_id++;
   s.state = 1;
@@ -115,6 +119,7 @@ int open_slot(wgcs_stager* st, uint32_t idx) {
 }
 
 int stage(wgcs_stager* st, size_t max_n, uint8_t** dst, int* read_idx) {
+  if (st->broken) return set_err(st->ctx, WGCS_ERR_HIP, "stager unusable after a HIP error");
   Slot& s = st->slots[st->open];
   if (s.reserved >= 0) return set_err(st->ctx, WGCS_ERR_INVALID_ARG, "stager: commit the open reservation first");
   if (s.carry) return set_err(st->ctx, WGCS_ERR_BATCH_FULL, "stager: a committed read waits for submit");
@@ -273,6 +278,7 @@ int wgcs_stager_commit(wgcs_stager* st, int read_idx, size_t n) {
 int wgcs_stager_submit(wgcs_stager* st, uint64_t* batch) {
   if (!st || !batch) return WGCS_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(st->mu);
+  if (st->broken) return set_err(st->ctx, WGCS_ERR_HIP, "stager unusable after a HIP error");
   hipSetDevice(st->ctx->device);
   Slot& s = st->slots[st->open];
   if (s.reserved >= 0) return set_err(st->ctx, WGCS_ERR_INVALID_ARG, "stager: open reservation");
@@ -301,6 +307,9 @@ int wgcs_stager_submit(wgcs_stager* st, uint64_t* batch) {
   const size_t carry = s.carry;
   const uint8_t* carry_src = s.h_in + s.used_in;  // not part of this batch's H2D
   int rc = open_slot(st, (st->open + 1) % st->depth);
+  if (rc && carry)  // the batch went out without the carried read, and no slot is open to take it
+    return set_err(st->ctx, rc, "stager: ring slot not reopened (HIP error): the read committed with "
+                                "BATCH_FULL (%zu bytes) was NOT staged; the stager is unusable", carry);
   if (rc || !carry) return rc;
   Slot& t = st->slots[st->open];
   memcpy(t.h_in, carry_src, carry);

@@ -28,6 +28,9 @@ int ensure_dev(wgcs_ctx* ctx, DevBuf& b, size_t bytes);
 int ensure_pinned(wgcs_ctx* ctx, HostBuf& b, size_t bytes);
 // [p, p + n) lies inside one wgcs_host_alloc allocation of ctx
 bool host_mapped(wgcs_ctx* ctx, const void* p, size_t n);
+// A live write-stager slot (open, or submitted and not yet finished) still
+// reads [a, b) through a zero-copy push (wstager.cpp); caller holds host_mu.
+bool wstager_references(wgcs_wstager* ws, uintptr_t a, uintptr_t b);
 
 }  // namespace wgcs
 
@@ -42,7 +45,11 @@ struct wgcs_ctx {
   wgcs::DevBuf d_arena, d_pkts, d_init, d_out, d_out2, d_aux;
   // pinned host staging
   wgcs::HostBuf h_stage, h_meta, h_out;
-  // wgcs_host_alloc allocations (device-readable pinned memory): [start, end)
+  // stream-join events of wgcs_checksum_batches (timing disabled), created on first use
+  hipEvent_t join_ev[WGCS_MAX_BATCH_STREAMS] = {};
+  // wgcs_host_alloc allocations (device-readable pinned memory): [start, end),
+  // and the live write stagers, whose zero-copy pushes point into them
   std::mutex host_mu;
   std::vector<std::pair<uintptr_t, uintptr_t>> host_allocs;
+  std::vector<wgcs_wstager*> wstagers;
 };

@@ -119,6 +119,7 @@ struct wgcs_wstager {
   std::vector<WSlot> slots;
   uint32_t open = 0;
   uint64_t next_id = 1;
+  bool broken = false;  // a ring slot could not be opened (HIP error): every later call fails
   std::mutex mu;
   std::condition_variable copied;  // a push finished copying into its slot
   WSlot* find(uint64_t id) {
@@ -142,11 +143,19 @@ void free_wslot(WSlot& s) {
   s = WSlot();
 }
 
+// Device arena bytes one slot may stage (the slices of its calls; each slice
+// holds its capped capacity, arena_need): a push that would pass it is
+// BATCH_FULL, or INVALID_ARG for a call that alone exceeds it.
+constexpr uint64_t kMaxArena = 8ull << 30;
+
 int open_wslot(wgcs_wstager* ws, uint32_t idx) {
   WSlot& s = ws->slots[idx];
   if (s.state == 2) {
     hipError_t e = hipEventSynchronize(s.done);
-    if (e != hipSuccess) return hip_fail(ws->ctx, e, "wstager: wait for ring slot");
+    if (e != hipSuccess) {
+      ws->broken = true;  // ws->open still names the submitted slot: nothing may be pushed into it
+      return hip_fail(ws->ctx, e, "wstager: wait for ring slot (stager unusable)");
+    }
   }
   s.id = ws->next_id++;
   s.state = 1;
@@ -161,6 +170,22 @@ int open_wslot(wgcs_wstager* ws, uint32_t idx) {
 }
 
 }  // namespace
+
+namespace wgcs {
+
+bool wstager_references(wgcs_wstager* ws, uintptr_t a, uintptr_t b) {
+  std::lock_guard<std::mutex> g(ws->mu);
+  for (const WSlot& s : ws->slots) {
+    if (s.state != 1 && !(s.state == 2 && hipEventQuery(s.done) == hipErrorNotReady)) continue;
+    for (uint32_t k = 0; k < s.npk; ++k) {
+      const WsMove& m = s.h_moves[k];
+      if ((m.flags & WS_MOVE_ABS) && m.src < b && m.src + 16ull * m.n16 > a) return true;
+    }
+  }
+  return false;
+}
+
+}  // namespace wgcs
 
 extern "C" {
 
@@ -212,12 +237,21 @@ int wgcs_wstager_create(wgcs_ctx* ctx, uint32_t depth, uint32_t max_writes, uint
     delete ws;
     return rc;
   }
+  {
+    std::lock_guard<std::mutex> g(ctx->host_mu);
+    ctx->wstagers.push_back(ws);
+  }
   *out = ws;
   return WGCS_OK;
 }
 
 int wgcs_wstager_destroy(wgcs_wstager* ws) {
   if (!ws) return WGCS_ERR_INVALID_ARG;
+  {
+    std::lock_guard<std::mutex> g(ws->ctx->host_mu);
+    auto& v = ws->ctx->wstagers;
+    v.erase(std::remove(v.begin(), v.end(), ws), v.end());
+  }
   hipSetDevice(ws->ctx->device);
   for (auto& s : ws->slots) {
     if (s.state == 2) hipEventSynchronize(s.done);
@@ -254,7 +288,8 @@ int push_call(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, 
       break;
     }
   size_t need = 0, need_out = 0, total = 0;
-  if (!c.status)
+  uint64_t need_arena = 0;
+  if (!c.status) {
     for (int i = 0; i < n; ++i) {
       if (caps[i] < lens[i]) return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: cap(bufs[%d]) < len", i);
       total += lens[i] - offset;
@@ -263,11 +298,17 @@ int push_call(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, 
       if (!pinned) need += kHead + al16(lens[i] - offset);
       need_out += out_need(lens[i] - offset);
     }
+    for (int i = 0; i < n; ++i) need_arena += arena_need((size_t)offset, std::min(caps[i], (size_t)offset + total));
+    if (need_arena > kMaxArena)
+      return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: one Write call needs %llu arena bytes (at most %llu)",
+                     (unsigned long long)need_arena, (unsigned long long)kMaxArena);
+  }
   uint8_t* stage;
   uint64_t at;
   WSlot* sp;
   {
     std::lock_guard<std::mutex> g(ws->mu);
+    if (ws->broken) return set_err(ws->ctx, WGCS_ERR_HIP, "wstager unusable after a HIP error");
     WSlot& s = ws->slots[ws->open];
     if (s.calls.size() >= ws->max_writes) return set_err(ws->ctx, WGCS_ERR_BATCH_FULL, "wstager: open batch is full");
     if (c.status || n == 0) {
@@ -275,7 +316,8 @@ int push_call(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, 
       s.calls.push_back(c);
       return WGCS_OK;
     }
-    if (s.npk + (uint32_t)n > ws->max_pkts || s.used + need > ws->max_bytes || s.out_used + need_out > ws->max_out) {
+    if (s.npk + (uint32_t)n > ws->max_pkts || s.used + need > ws->max_bytes || s.out_used + need_out > ws->max_out ||
+        s.arena + need_arena > kMaxArena) {
       if (s.npk == 0)  // would never fit, even in an empty slot: not a BATCH_FULL the caller can retry
         return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: one Write call exceeds max_pkts / max_bytes");
       return set_err(ws->ctx, WGCS_ERR_BATCH_FULL, "wstager: open batch is full");
@@ -363,8 +405,13 @@ int wgcs_wstager_submit(wgcs_wstager* ws, uint64_t* batch) {
   if (!ws || !batch) return WGCS_ERR_INVALID_ARG;
   std::unique_lock<std::mutex> g(ws->mu);
   hipSetDevice(ws->ctx->device);
+  // Wait for the pushes still copying into the open slot.  The wait releases
+  // the lock, so another submit may queue that slot meanwhile: re-read
+  // ws->open after every wake-up and submit whatever slot is open then (each
+  // submit queues a distinct slot; none is skipped or queued twice).
+  ws->copied.wait(g, [&] { return ws->broken || ws->slots[ws->open].copying == 0; });
+  if (ws->broken) return set_err(ws->ctx, WGCS_ERR_HIP, "wstager unusable after a HIP error");
   WSlot& s = ws->slots[ws->open];
-  ws->copied.wait(g, [&] { return s.copying == 0; });  // pushes still copying into this slot
   const hipStream_t q = s.stream;
   hipError_t e = hipSuccess;
   if (s.ndev) {

@@ -17,6 +17,7 @@ Every byte is processed by the gfx950 kernels in libwgcsum.so.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 
 import numpy as np
 
@@ -44,6 +45,9 @@ def pkt_off(pkts: np.ndarray) -> np.ndarray:
     """Arena offsets of a PKT_DTYPE array (uint64)."""
     return pkts["off_lo"].astype(np.uint64) | (pkts["off_hi"].astype(np.uint64) << np.uint64(32))
 GSO_JOB_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("pad", "<u4")])
+# wgcs_batch (include/wgcsum.h): one batch of wgcs_checksum_batches
+BATCH_DTYPE = np.dtype([("arena", "<u8"), ("pkts", "<u8"), ("initial", "<u8"), ("out", "<u8"), ("n", "<u4"),
+                        ("pad", "<u4")])
 # wgcs_gro_buf / wgcs_gro_call (include/wgcsum.h): a device-resident Tun.Write batch
 GRO_BUF_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("cap", "<u4")])
 GRO_CALL_DTYPE = np.dtype([("first", "<u4"), ("n", "<u4"), ("offset", "<i4"), ("flags", "<u4")])
@@ -95,9 +99,12 @@ class Device:
             raise WgcsError(rc, self.lib.wgcs_strerror(rc).decode())
         self.h = h
         self.device = device
+        self._stagers = weakref.WeakSet()  # closed before the context (wgcs_destroy refuses live write stagers)
 
     def close(self) -> None:
         if self.h:
+            for st in list(self._stagers):
+                st.close()
             self.lib.wgcs_destroy(self.h)
             self.h = None
 
@@ -144,6 +151,30 @@ class Device:
         s = getattr(stream, "cuda_stream", stream)
         self._check(self.lib.wgcs_checksum_batch(self.h, mode, F_INPLACE if inplace else 0, _ptr(arena), _ptr(pkts),
                                                  _ptr(initial), n, _ptr(out), s))
+
+    @staticmethod
+    def batch_list(batches) -> np.ndarray:
+        """wgcs_batch array for checksum_batches from (arena, pkts, n, out[,
+        initial]) tuples of device pointers / tensors."""
+        a = np.zeros(len(batches), BATCH_DTYPE)
+        for k, b in enumerate(batches):
+            arena, pkts, n, out = b[:4]
+            a[k] = (_ptr(arena), _ptr(pkts), _ptr(b[4]) if len(b) > 4 and b[4] is not None else 0, _ptr(out), n, 0)
+        return a
+
+    def checksum_batches(self, mode: int, batches: np.ndarray, streams=(), ev_begin=None, ev_end=None,
+                         inplace: bool = False) -> None:
+        """Enqueue a series of independent batches with one call
+        (wgcs_checksum_batches): batches[k] (a batch_list array) on
+        streams[k % len(streams)]; ev_begin / ev_end (torch.cuda.Event or raw
+        hipEvent_t) bracket every launch."""
+        ss = (C.c_void_p * max(len(streams), 1))(*[getattr(s, "cuda_stream", s) for s in streams])
+        evb = getattr(ev_begin, "cuda_event", ev_begin)
+        eve = getattr(ev_end, "cuda_event", ev_end)
+        if (ev_begin is not None and not evb) or (ev_end is not None and not eve):
+            raise ValueError("bracket event has no HIP event yet (torch creates it on its first record)")
+        self._check(self.lib.wgcs_checksum_batches(self.h, mode, F_INPLACE if inplace else 0, batches.ctypes.data,
+                                                   len(batches), ss, len(streams), evb or None, eve or None))
 
     def gso_split_batch(self, arena, jobs, n_jobs: int, out, out_stride: int, offset: int, max_segs: int, sizes,
                         count, status, stream=None) -> None:
@@ -259,6 +290,7 @@ class Stager:
         h = C.c_void_p()
         dev._check(self.lib.wgcs_stager_create(dev.h, depth, max_reads, max_bytes, max_segs, seg_room, C.byref(h)))
         self.h = h
+        dev._stagers.add(self)
         self.max_segs = max_segs
 
     def close(self) -> None:
@@ -340,6 +372,7 @@ class WriteStager:
         h = C.c_void_p()
         dev._check(self.lib.wgcs_wstager_create(dev.h, depth, max_writes, max_pkts, max_bytes, C.byref(h)))
         self.h = h
+        dev._stagers.add(self)
         self._n = {}
 
     def close(self) -> None:
