@@ -69,7 +69,12 @@ def parse():
                     help="gro_staged: host threads pushing Write calls concurrently (default 4)")
     ap.add_argument("--pinned", action="store_true",
                     help="gro_staged: Write buffers in pinned host memory, zero-copy pushes")
+    ap.add_argument("--max-segs", type=int, default=128,
+                    help="cfg4: output slots per read = len(bufs) (the reference's Read passes conn.BatchSize = 128)")
     ap.add_argument("--verify", action="store_true", help="check the GPU results against the synth ground truth")
+    ap.add_argument("--repeat", type=int, default=1,
+                    help="diagnostics: time the K-step region this many times; `value` stays the FIRST region, "
+                         "the others are listed under timing.repeats")
     return ap.parse_args()
 
 
@@ -194,9 +199,6 @@ def main():
     def batches(K, k0):  # steps k0 .. k0+K-1: each its own rotated arena and output
         return dev.batch_list([(arenas[(k0 + k) % R], pkts, n, outs[(k0 + k) % R]) for k in range(K)])
 
-    def step(k, ns=S):
-        dev.checksum_batches(mode, batches(1, k), streams[k % ns: k % ns + 1])
-
     # The K steps are enqueued by ONE library call (wgcs_checksum_batches: step k
     # on stream k % S), which also records the HIP bracket events on the launch
     # streams: e0 on stream 0 before the first launch (the others wait on it),
@@ -229,11 +231,14 @@ def main():
     iso_first = os.environ.get("WGCS_ISO_FIRST", "1") == "1"
     iso_ms = None
     if use_events and S > 1 and iso_first:
-        for k in range(min(args.warmup, 5)):
-            step(k, 1)
+        dev.checksum_batches(mode, batches(min(args.warmup, 5), 0), streams[:1])
         _, iso_ms = timed(max(args.steps, 20), 0, 1)
-    for k in range(args.warmup):
-        step(k)
+    # W warmup steps, enqueued exactly as the timed steps are (one call, the
+    # same streams, the same bracket events): the first cross-stream wait and
+    # join on a stream costs ~40 us once per process (profiles/r3_probe_first_region.txt)
+    if args.warmup > 0:
+        dev.checksum_batches(mode, batches(args.warmup, 0), streams, e0 if use_events else None,
+                             e1 if use_events else None)
     torch.cuda.synchronize()
     if args.verify:
         if mode == MODE_VALIDATE:
@@ -246,6 +251,7 @@ def main():
             assert np.array_equal(got, want), "L4_FILL mismatch vs stored checksums"
 
     local_elapsed, kern_ms = timed(args.steps, args.warmup, S)
+    repeats = [timed(args.steps, args.warmup + r * args.steps, S) for r in range(1, args.repeat)]
     elapsed = shard.max_over_ranks(local_elapsed, dist, device=red_dev)
     if use_events and S > 1 and not iso_first:  # reference: the same launches one at a time on one stream (untimed for `value`)
         _, iso_ms = timed(max(args.steps, 20), args.warmup + args.steps, 1)
@@ -290,6 +296,9 @@ def main():
         result["timing"] = {"wall_us": round(local_elapsed * 1e6, 2), "event_span_us": round(kern_ms * args.steps * 1e3, 2),
                             "wall_minus_span_us": round((local_elapsed - kern_ms * args.steps * 1e-3) * 1e6, 2),
                             "enqueue": "one wgcs_checksum_batches call for the K steps"}
+        if repeats:
+            result["timing"]["repeats"] = [{"wall_us": round(w * 1e6, 1), "event_span_us": round(m * args.steps * 1e3, 1)}
+                                           for w, m in repeats]
         achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
         result["roofline"] = {
             "bound": "hbm",
@@ -444,6 +453,17 @@ def _time_oracle(oracle, mode, arena_np, pkts_np, threads, seconds):
     return reps, time.perf_counter() - t0
 
 
+def _go_note() -> str:
+    """north_star asks for the pure-Go CPU baseline: say whether a Go toolchain
+    exists on this host (none on the GPU boxes: profiles/r3_go_probe.txt)."""
+    import shutil
+
+    found = [t for t in ("go", "gccgo", "tinygo") if shutil.which(t)]
+    if found:
+        return f"Go toolchain present ({', '.join(found)}) but no pure-Go leg is built"
+    return "no Go toolchain on this host (go, gccgo, tinygo absent), so the pure-Go baseline cannot run here"
+
+
 def cpu_baseline(arena_np, pkts_np, mode, seconds):
     """The oracle (C restatement of tun/checksum.go) on the same batch: one
     thread for `seconds`, plus an all-host-cores leg for a quarter of that --
@@ -471,7 +491,8 @@ def cpu_baseline(arena_np, pkts_np, mode, seconds):
         "cores": 1,
         "kind": "port",
         "sample": f"{reps} passes over the same {len(pkts_np)}-frame batch ({nbytes/1e6:.1f} MB), "
-                  f"{dt:.1f} s, C -O3 restatement of tun/checksum.go + checksumValid, 1 thread",
+                  f"{dt:.1f} s, C -O3 restatement of tun/checksum.go + checksumValid, 1 thread; "
+                  + _go_note(),
         "all_cores": dict(mt, unit="GiB/s", cores=threads, host_nproc=os.cpu_count()),
     }
 

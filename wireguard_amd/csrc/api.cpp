@@ -112,7 +112,14 @@ int wgcs_init(int device, wgcs_ctx** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault);
   hipDeviceProp_t prop;
   if (e == hipSuccess) e = hipGetDeviceProperties(&prop, device);
+  // stream-join events of wgcs_checksum_batches, made here so that no event is
+  // created inside a caller's timed enqueue
+  for (int j = 1; j < WGCS_MAX_BATCH_STREAMS && e == hipSuccess; ++j)
+    e = hipEventCreateWithFlags(&ctx->join_ev[j], hipEventDisableTiming);
   if (e != hipSuccess) {
+    for (hipEvent_t ev : ctx->join_ev)
+      if (ev) hipEventDestroy(ev);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
     return WGCS_ERR_HIP;
   }
@@ -265,10 +272,6 @@ int wgcs_checksum_batches(wgcs_ctx* ctx, int mode, unsigned flags, const wgcs_ba
   hipStream_t st[WGCS_MAX_BATCH_STREAMS];
   for (uint32_t j = 0; j < ns; ++j) st[j] = n_streams && streams[j] ? (hipStream_t)streams[j] : ctx->stream;
   hipError_t e = hipSuccess;
-  if (ev_end)
-    for (uint32_t j = 1; j < ns && e == hipSuccess; ++j)
-      if (!ctx->join_ev[j]) e = hipEventCreateWithFlags(&ctx->join_ev[j], hipEventDisableTiming);
-  if (e != hipSuccess) return hip_fail(ctx, e, "hipEventCreate");
   // ev_begin, then batch 0 at once (the first launch is the latency-critical
   // one); each other stream waits on ev_begin just before its first launch
   if (ev_begin && (e = hipEventRecord((hipEvent_t)ev_begin, st[0])) != hipSuccess) return hip_fail(ctx, e, "ev_begin");

@@ -839,6 +839,9 @@ __device__ __noinline__ void decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, 
 #ifndef WGCS_GSO_WAVES
 #define WGCS_GSO_WAVES 5
 #endif
+#ifndef WGCS_GSO_GROUPS
+#define WGCS_GSO_GROUPS 3  // blocks per job (grid y); each takes every WGCS_GSO_GROUPS-th segment group
+#endif
 template <int U, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WAVES, 8))) void gso_rows_kernel(const uint8_t* __restrict__ arena,
                                                        const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
@@ -864,13 +867,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
     obase = outpos[jb].base;
     opitch = outpos[jb].pitch;
   }
-  const int segb = (int)(blockIdx.y * (uint32_t)ROWS);
-  const int i = segb + wv * 4 + (lane >> 4);  // this row's segment
-  uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
-  const int dalign = (int)((uintptr_t)dst & 15u);
-  uint8_t* dbase = dst - dalign;
-  const uint4 z = make_uint4(0, 0, 0, 0);
-
   // ---- header chunks in packet coordinates (lane r of each row: the 16-byte
   // aligned chunks r and r + 1 from the one holding readBuf[0]), issued first:
   // they need only the descriptor.  Raw buffer loads over the job's bytes:
@@ -917,19 +913,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
                        fast_header(cs_s, hdr_s, ca_s, tcp_s) && (uint32_t)pkt0_s <= room;
   const int nfull_s = clean_s ? (plen_s - hdr_s + gso_s - 1) / gso_s : 0;
   const int nseg_s = min(nfull_s, (int)max_segs);
-  const bool live_s = clean_s && i < nseg_s;  // row-uniform
-  // A block past the job's last segment under every verdict retires now
-  // (callers size bufs for the largest read, conn.IdealBatchSize = 128
-  // slots, so most groups of a 64-KiB read are empty).  Group 0 always stays:
-  // it writes count / status and the GSO_NONE packet.  hdrLen >= csumStart +
-  // 20 (TCP, tun.go:608-613) or = csumStart + 8 (UDP) or the virtio value
-  // (raw jobs) bounds the segment count from above.
-  if (blockIdx.y > 0 && jlen >= 14) {
+  // Segment groups: this block takes groups blockIdx.y, + gridDim.y, ... of
+  // the job's ceil(max_segs / 16).  The grid has only a few blocks per job
+  // (callers size bufs for the largest read, conn.IdealBatchSize = 128 slots,
+  // so most groups of a 64-KiB read are empty): groups past the job's last
+  // segment under every verdict cost no dispatch and are never entered.
+  // hdrLen >= csumStart + 20 (TCP, tun.go:608-613) or = csumStart + 8 (UDP) or
+  // the virtio value (raw jobs) bounds the segment count from above.  Group 0
+  // always runs: it writes count / status and the GSO_NONE packet.
+  const int ngroups = (int)((max_segs + ROWS - 1) / ROWS);
+  int gbound = ngroups;  // groups that may hold a segment
+  if (jlen >= 14) {
     const int hmin = raw ? (int)hl : (tcp_s ? cs_s + 20 : cs_s + 8);
     const bool split_type = ok_s && cs_s + 60 <= 0xFFFF;
-    const int nbound = !split_type ? INT32_MAX : (plen_s > hmin ? (plen_s - hmin + gso_s - 1) / gso_s : 0);
-    if ((!raw && t1 == GSO_NONE) || (split_type && segb >= nbound)) return;
+    if (!raw && t1 == GSO_NONE) {
+      gbound = 1;
+    } else if (split_type) {
+      const int nbound = plen_s > hmin ? (plen_s - hmin + gso_s - 1) / gso_s : 0;
+      gbound = max(1, min(ngroups, (nbound + ROWS - 1) / ROWS));
+    }
   }
+  if ((int)blockIdx.y >= gbound) return;
 
   uint4 Q = funnel(H0, H1, hph);  // readBuf[16r, 16r + 16) (bytes below hdrLen)
   // the TCP data offset decides hdrLen (tun.go:601-614): block-uniform verdict
@@ -949,17 +953,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
       count[jb] = many ? (int)max_segs - 1 : nfull_s;
       status[jb] = many ? WGCS_ERR_TOO_MANY_SEGMENTS : 0;
     }
-    if (live_s) {
-      // ---- the payload stream
-      const int type = type_s, ipv = ipv_s, hdr_len = hdr_s, gso = gso_s, cs = cs_s, co = co_s, plen = plen_s;
-      uint32_t acc = 0;
-      stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen));
-      uint32_t ip_base = 0, l4_base = 0, tflags = 0, id0 = 0, seq0 = 0;
-      {
-      // job-constant header sums from this row's own header chunks (header_fast's
-      // values): IPv4 header without total length / id / checksum, the L4
-      // header from csumStart without checksum field, seq / UDP length and the
-      // flags byte, and the pseudo-header addresses, each as BE words
+    const int type = type_s, ipv = ipv_s, hdr_len = hdr_s, gso = gso_s, cs = cs_s, co = co_s, plen = plen_s;
+    // job-constant header sums from this row's own header chunks (header_fast's
+    // values): IPv4 header without total length / id / checksum, the L4
+    // header from csumStart without checksum field, seq / UDP length and the
+    // flags byte, and the pseudo-header addresses, each as BE words
+    uint32_t ip_base = 0, l4_base = 0, tflags = 0, id0 = 0, seq0 = 0;
+    {
       const int x0 = 16 * r;
       const bool tcp_c = type != GSO_UDP_L4;
       const int vlo = cs + 4, vhi = tcp_c ? cs + 8 : cs + 6;
@@ -980,13 +980,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
       l4_base = (uint32_t)ufl((int)t4) + (tflags & ~0x09u);
       if (ipv == 4) id0 = (qbyte(Q, 4) << 8) | qbyte(Q, 5);
       if (tcp_c) seq0 = (qbyte(Q, vlo) << 24) | (qbyte(Q, vlo + 1) << 16) | (qbyte(Q, vlo + 2) << 8) | qbyte(Q, vlo + 3);
+    }
+    for (int grp = (int)blockIdx.y; grp * ROWS < nseg_s; grp += (int)gridDim.y) {  // block-uniform
+      const int i = grp * ROWS + wv * 4 + (lane >> 4);  // this row's segment
+      if (i < nseg_s) {  // row-uniform
+        uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
+        const int dalign = (int)((uintptr_t)dst & 15u);
+        uint8_t* dbase = dst - dalign;
+        // ---- the payload stream
+        uint32_t acc = 0;
+        stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen));
+        finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
+                   tflags, id0, seq0, &sizes[slot0 + (uint32_t)i]);
       }
-      finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base, tflags,
-                 id0, seq0, &sizes[slot0 + (uint32_t)i]);
     }
   } else {
-    decoded_rows<U, NT>(vb, jlen, job.flags, room, max_segs, i, blockIdx.y == 0, &count[jb], &status[jb],
-                        out + obase + offset, dst, &sizes[slot0]);
+    for (int grp = (int)blockIdx.y; grp < gbound; grp += (int)gridDim.y) {  // block-uniform
+      const int i = grp * ROWS + wv * 4 + (lane >> 4);
+      uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
+      decoded_rows<U, NT>(vb, jlen, job.flags, room, max_segs, i, grp == 0, &count[jb], &status[jb],
+                          out + obase + offset, dst, &sizes[slot0]);
+      lds_barrier();  // every wave is done with this group's verdict before the next one is published
+    }
   }
 }
 
@@ -996,8 +1011,10 @@ hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs
                                   uint32_t room) {
   if (n_jobs == 0 || max_segs == 0) return hipSuccess;
   if (!outpos) room = out_stride > offset ? out_stride - offset : 0;
-  const uint32_t gy = (max_segs + 15) / 16;  // 16 segments (4 waves) per block
-  if (gy > 65535u) return hipErrorInvalidValue;
+  // 16 segments (4 waves) per block and group; a few blocks per job, each
+  // looping over its groups (a 65,535-B read at MSS 1460 has 3 groups)
+  const uint32_t ngroups = (max_segs + 15) / 16;
+  const uint32_t gy = ngroups < (uint32_t)WGCS_GSO_GROUPS ? ngroups : (uint32_t)WGCS_GSO_GROUPS;
   hipLaunchKernelGGL((gso_rows_kernel<WGCS_GSO_U, true>), dim3(n_jobs, gy), dim3(256), 0, s, arena, jobs, max_segs, out,
                      out_stride, outpos, offset, room, sizes, count, status);
   return hipGetLastError();

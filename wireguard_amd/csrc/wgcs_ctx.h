@@ -45,7 +45,7 @@ struct wgcs_ctx {
   wgcs::DevBuf d_arena, d_pkts, d_init, d_out, d_out2, d_aux;
   // pinned host staging
   wgcs::HostBuf h_stage, h_meta, h_out;
-  // stream-join events of wgcs_checksum_batches (timing disabled), created on first use
+  // stream-join events of wgcs_checksum_batches (timing disabled; [1, 16) made by wgcs_init)
   hipEvent_t join_ev[WGCS_MAX_BATCH_STREAMS] = {};
   // wgcs_host_alloc allocations (device-readable pinned memory): [start, end),
   // and the live write stagers, whose zero-copy pushes point into them

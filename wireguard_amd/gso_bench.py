@@ -21,7 +21,9 @@ HBM_PEAK_GBS = 8000.0
 
 def run(args, torch, dev, dist, rank, world, local, barrier):
     n_jobs, total, gso = 256, 65535, 1460
-    max_segs, stride, offset = 64, 1536, 16
+    # output slots per read: len(bufs) of the reference's Read = conn.BatchSize = 128
+    # (/root/reference/device/send.go:239-245, tun/tun.go:870); --max-segs 64 for the round-2 line
+    max_segs, stride, offset = getattr(args, "max_segs", 128), 1536, 16
     R = max(args.rotate, 8)  # (16.8 MB in + 25 MB out) per copy: rotate past the 256 MiB MALL
     pkts = [synth.make_super_packet(total, gso, seed=synth.SEED + 1000 * rank + k) for k in range(n_jobs)]
     jlen = len(pkts[0])
@@ -45,16 +47,6 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
         dev.gso_split_batch(d_arena[i], d_jobs, n_jobs, d_out[i], stride, offset, max_segs, d_sizes[q], d_count[q],
                             d_status[q], stream=streams[q])
 
-    for k in range(args.warmup):
-        step(k)
-    torch.cuda.synchronize()
-    count = d_count[0].cpu().numpy()
-    status = d_status[0].cpu().numpy()
-    assert (status == 0).all() and (count == 45).all(), (status[:4], count[:4])
-    sizes = d_sizes[0].cpu().numpy().reshape(n_jobs, max_segs)
-    bytes_out = int(sizes.astype(np.int64).sum())
-    bytes_in = int(jobs["len"].astype(np.int64).sum())
-    bytes_per_step = bytes_in + bytes_out
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     joins = [torch.cuda.Event() for _ in streams[1:]]
@@ -76,6 +68,16 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
         barrier()
         return time.perf_counter() - t0, e0.elapsed_time(e1) / K
 
+    if args.warmup > 0:  # the W warmup steps go through the same bracket as the timed ones
+        timed(args.warmup, 0, S)
+    torch.cuda.synchronize()
+    count = d_count[0].cpu().numpy()
+    status = d_status[0].cpu().numpy()
+    assert (status == 0).all() and (count == 45).all(), (status[:4], count[:4])
+    sizes = d_sizes[0].cpu().numpy().reshape(n_jobs, max_segs)
+    bytes_out = int(sizes.astype(np.int64).sum())
+    bytes_in = int(jobs["len"].astype(np.int64).sum())
+    bytes_per_step = bytes_in + bytes_out
     elapsed, kern_ms = timed(args.steps, args.warmup, S)
     elapsed = shard.max_over_ranks(elapsed, dist)
     iso_ms = timed(max(args.steps, 20), args.warmup + args.steps, 1)[1] if S > 1 else None
@@ -111,6 +113,7 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
             "workload": "256 x 65535-B TCP/IPv4 super-packets -> 45 x <=1500-B segments each (gsoSize 1460), "
                         "BASELINE.json configs[3]",
             "segments_per_step": int((count).sum()),
+            "max_segs": max_segs,
             "bytes_in": bytes_in,
             "bytes_out": bytes_out,
             "rotated_copies": R,
@@ -125,6 +128,7 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic.per_launch("gso_rows_kernel<6,true>", bytes_per_step),
             "kernel": "gso_rows_kernel<6,true>",
+            "grid": f"({n_jobs}, {min((max_segs + 15) // 16, 3)}) blocks of 256: one block per (job, group lane), looping over segment groups",
             "kernel_ms": round(kern_ms, 5),
             "kernel_ms_is": ("GPU time per launch over the timed region (HIP events on the launch streams)"
                              + (f"; {S} streams, consecutive launches overlap" if S > 1 else "")),
