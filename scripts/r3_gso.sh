@@ -12,3 +12,7 @@ fi
 for ms in 128 64; do
   for rep in 1 2; do step cfg4_${ms}_$rep 200 python bench.py --config cfg4 --max-segs $ms --steps 100 --warmup 10 --cpu-seconds 0 --no-e2e; summ cfg4_${ms}_$rep; done
 done
+if [ "${SQ:-0}" = 1 ]; then
+  (cd /tmp && step sq 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -d $OUT/sq -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --config cfg4 --steps 20 --warmup 2 --cpu-seconds 0 --no-e2e --streams 1)
+  python3 scripts/pmc_summary.py $OUT/sq 2>/dev/null | tail -20 || true
+fi

@@ -509,20 +509,27 @@ __device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t rs, int off) {
 // One batch of dword-aligned windows: lane r loads windows k0 + r + 16u at job
 // offset aoff + 16 * window (lane 15 also the first dword of the window after
 // the batch, E), each only when it overlaps the job bytes [lo, hi).
+// A window that is not needed gets an offset past the resource's range instead
+// of a branch around its load: the range check returns zeros and touches no
+// memory, so the loads are issued unconditionally (no exec-mask branches, and
+// the compiler can wait on them one by one with vmcnt(n)).
+constexpr int kOobOffset = 0x7FFFFFF0;
 template <int U, bool NT>
 __device__ __forceinline__ void load_windows(__amdgpu_buffer_rsrc_t rs, int aoff, int k0, int r, int lo, int hi,
                                              uint4 (&A)[U], uint32_t& E) {
-  const uint4 z = make_uint4(0, 0, 0, 0);
   const int o0 = aoff + 16 * (k0 + r);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int o = o0 + 256 * u;
-    A[u] = (o < hi && o + 16 > lo) ? bld16<NT>(rs, o) : z;
+    A[u] = bld16<NT>(rs, (o < hi && o + 16 > lo) ? o : kOobOffset);
   }
-  E = 0;
   const int oe = aoff + 16 * (k0 + 16 * U);
-  if (r == 15 && oe < hi && oe + 4 > lo) E = __builtin_amdgcn_raw_buffer_load_b32(rs, oe, 0, NT ? 2 : 0);
+  E = __builtin_amdgcn_raw_buffer_load_b32(rs, (r == 15 && oe < hi && oe + 4 > lo) ? oe : kOobOffset, 0,
+                                           NT ? 2 : 0);
 }
+
+// Wave-uniform: no lane of the wave has `pred` set (a scalar compare, no exec-mask branch).
+__device__ __forceinline__ bool wave_none(bool pred) { return __builtin_amdgcn_ballot_w64(pred) == 0; }
 
 // One row's payload stream: destination chunk k = bytes [sb, sb + 16) of the
 // dword-aligned source window k and the first dword of window k + 1 (next
@@ -552,12 +559,19 @@ __device__ __forceinline__ void stream_row(const uint8_t* rb, int i, int gso, in
       const uint32_t Rx = u + 1 < U ? row_next(A[u + 1 < U ? u + 1 : u].x) : E;
       const uint32_t nx = r == 15 ? Rx : Rc;
       Rc = Rx;
-      if (k < nk) {
-        const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(A[u].y, A[u].x, sb),
-                                   __builtin_amdgcn_alignbyte(A[u].z, A[u].y, sb),
-                                   __builtin_amdgcn_alignbyte(A[u].w, A[u].z, sb),
-                                   __builtin_amdgcn_alignbyte(nx, A[u].w, sb));
-        const int x0 = 16 * k - dalign;
+      const int x0 = 16 * k - dalign;
+      const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(A[u].y, A[u].x, sb),
+                                 __builtin_amdgcn_alignbyte(A[u].z, A[u].y, sb),
+                                 __builtin_amdgcn_alignbyte(A[u].w, A[u].z, sb),
+                                 __builtin_amdgcn_alignbyte(nx, A[u].w, sb));
+      if (wave_none(x0 < hdr_len || x0 + 16 > pkt_len)) {
+        // every chunk of this step in every row of the wave is whole payload
+        // (the bulk of a segment): unmasked sum and a full store, no branches
+        acc = add4(acc, v);
+        int ko = 16 * k;
+        asm volatile("" : "+v"(ko));
+        *reinterpret_cast<uint4*>(dbase + ko) = v;
+      } else if (k < nk) {
         if (x0 >= hdr_len && x0 + 16 <= pkt_len) acc = add4(acc, v);
         else acc = add4_masked(acc, v, byte_bits16(hdr_len - x0, pkt_len - x0), false);
         // the chunk's address formed here, not hoisted for all U chunks up front
