@@ -39,6 +39,8 @@ def bench_key(k):
     m = re.search(r"gso_rows_kernel<(\d+), (true|false)(?:, (\d+))?>", k)
     if m:  # round 1 / early round 2 had a third template argument (block waves)
         return f"gso_rows_kernel<{m.group(1)},{m.group(2)}" + (f",{m.group(3)}>" if m.group(3) else ">")
+    if "gro_batch_kernel" in k:
+        return "gro_batch_kernel"
     m = re.search(r"udp_split_kernel<(\d+)>", k)
     if m:
         return f"udp_split_kernel<{m.group(1)}>"

@@ -246,3 +246,12 @@ def test_gro_batch_tcp_options_fuzz(dev):
         cap = 65535 if k % 4 else (lambda n, e=int(rng.integers(0, 4000)): OFFSET + n + e)
         calls.append((pk, cap, bool(k % 5), None))
     assert _check(dev, calls) == len(calls)
+
+
+def test_gro_batch_bench_call_shapes(dev):
+    """The gro_device bench's call shapes (one 128-packet flow, prepend chains,
+    a shuffled batch) against the oracle, every byte, in one launch."""
+    from wireguard_amd.gro_bench import CALL_SHAPES, CAP, shape_batch
+
+    calls = [(shape_batch(dev, s), CAP, True, None) for s in CALL_SHAPES]
+    assert _check(dev, calls) == len(calls)

@@ -52,7 +52,10 @@ struct GroSmem {
   uint64_t boff[kMaxB];                 // arena offset of each original buffer
   uint32_t blen[kMaxB], bcap[kMaxB];    // its slice length / capacity
   uint32_t seq[kMaxB], ipattr[kMaxB], keyh[kMaxB], opth[kMaxB];
-  uint32_t kw[kMaxB][10];               // flow key words: addresses, ports, ack (TCP)
+  union {
+    uint32_t kw[kMaxB][10];  // step 2: flow key words (addresses, ports, ack for TCP)
+    uint4 rec[kMaxB];        // step 3: the walker's per-packet record (PktRec), one ds_read_b128
+  };
   uint32_t slen[kMaxB];                 // len(bufs[s]) of the slice now at position s
   uint32_t it_seq[kMaxB];
   uint32_t m_pos[kMaxB];            // materializations: first byte of the pieces in the buffer
@@ -243,9 +246,12 @@ struct Planner {
   struct TailCache {
     int it, s, tgt, stail, scount;
     uint32_t l4h, iphit, ipattr, g, nm, seq, psh, slen, cap, valid_s;
+    bool dirty;  // running fields newer than LDS
+    bool mult;   // the item's payload is a multiple of its gsoSize
   };
 
   __device__ void load_tail(TailCache& c, int f) const {
+    c.dirty = false;
     c.it = S.fl_tail[f];
     if (c.it == kNone) return;
     const int it = c.it;
@@ -264,45 +270,61 @@ struct Planner {
     c.stail = S.stail[s];
     c.scount = S.scount[s];
     c.ipattr = S.ipattr[c.tgt];
+    c.mult = c.g != 0 && ((int)c.slen - offset - (int)(uint8_t)(c.iphit + c.l4h)) % (int)c.g == 0;
   }
 
   // tcpGRO when packet bi appends to the flow's last item -- the in-order
   // bulk case: tcpPacketsCanCoalesce's append branch and coalesceTCPPackets'
   // checks (gro.go:433-512, :709-734) in the reference's order for that item,
-  // from registers instead of a chain of dependent LDS reads.  Returns false
-  // whenever any of them fails (or TCP options are present), and the general
-  // path (tcp_gro) then decides from LDS exactly as before.
-  __device__ bool tcp_append_fast(TailCache& c, int bi) {
+  // from registers: the item in `c`, the packet in its record R (PktRec, one
+  // LDS read, prefetched by the walker a step ahead).  Returns false whenever
+  // any of them fails (or TCP options are present), and the general path
+  // (tcp_gro) then decides from LDS exactly as before.  The item's running
+  // fields (tail, count, length, numMerged) stay in `c` until flush_tail.
+  __device__ bool tcp_append_fast(TailCache& c, int bi, const uint4& R) {
     if (c.it == kNone) return false;
-    const uint32_t th = S.th[bi], iph = S.iph[bi];
-    if (th != c.l4h || th > 20) return false;
-    if (S.ipattr[bi] != c.ipattr) return false;
+    const uint32_t th = R.w & 0xFFu, iph = (R.w >> 8) & 0xFFu;
+    const uint32_t gso = R.z & 0xFFFFu;
     const uint16_t lhs = (uint16_t)(c.g + (uint16_t)(c.g * c.nm));
-    if (S.seq[bi] != c.seq + (uint32_t)lhs) return false;
-    if (c.psh) return false;
+    // th == l4h and equal IP attributes (version included, so iph == the
+    // item's): the appended payload is the packet's gsoSize
     const int plen_s = (int)c.slen - offset;
-    if ((plen_s - (int)(iph + th)) % (int)c.g != 0) return false;
-    if (S.gso[bi] > c.g) return false;
-    const int pay = ((int)S.slen[bi] - offset) - (int)(uint8_t)(c.iphit + c.l4h);
-    if ((int)c.cap - offset < plen_s + pay) return false;  // coalesceInsufficientCap
-    if (c.nm == 0 && !c.valid_s) return false;             // coalesceItemInvalidCSum
-    if (!S.valid[bi]) return false;                        // coalescePktInvalidCSum
-    if (S.psh[bi]) {  // pktHead[iphLen+13] |= PSH (gro.go:724-729)
+    const int pay = (int)gso;
+    // every check of the append branch at once (no early exits: one lane
+    // walks, and each exit would be an exec-mask branch); c.mult is
+    // len(pktTarget[iphLen+tcphLen:]) % gsoSize == 0 (gro.go:479-484), kept
+    // incrementally instead of a division per packet
+    const bool ok = th == c.l4h && th <= 20 && R.y == c.ipattr && R.x == c.seq + (uint32_t)lhs && !c.psh &&
+                    c.mult && gso <= c.g && (int)c.cap - offset >= plen_s + pay &&  // coalesceInsufficientCap
+                    (c.nm != 0 || c.valid_s) &&                                      // coalesceItemInvalidCSum
+                    ((R.w >> 24) & 1u);                                              // coalescePktInvalidCSum
+    if (!ok) return false;
+    (void)iph;
+    if ((R.w >> 16) & 1u) {  // pktHead[iphLen+13] |= PSH (gro.go:724-729)
       S.it_psh[c.it] = 1;
       S.spsh[c.s] = 1;
       c.psh = 1;
     }
-    S.pstart[bi] = (uint16_t)(uint8_t)(c.iphit + c.l4h);
-    S.plen[bi] = (uint16_t)pay;
-    S.pnext[bi] = kNone;
+    S.pstart[bi] = (uint16_t)(c.iphit + c.l4h);
+    S.plen[bi] = (uint16_t)pay;  // S.pnext[bi] is kNone since step 1
     S.pnext[c.stail] = (int16_t)bi;
     c.stail = bi;
-    S.stail[c.s] = (int16_t)bi;
-    S.scount[c.s] = (int16_t)(++c.scount);
+    ++c.scount;
     c.slen += (uint32_t)pay;
-    S.slen[c.s] = c.slen;
-    S.it_nm[c.it] = (uint16_t)(++c.nm);
+    ++c.nm;
+    c.mult = pay == (int)c.g;  // a multiple before, so a multiple after iff this payload is gsoSize
+    c.dirty = true;
     return true;
+  }
+
+  // the item's running fields back into LDS (before the general path reads them)
+  __device__ void flush_tail(TailCache& c) {
+    if (!c.dirty) return;
+    S.stail[c.s] = (int16_t)c.stail;
+    S.scount[c.s] = (int16_t)c.scount;
+    S.slen[c.s] = c.slen;
+    S.it_nm[c.it] = (uint16_t)c.nm;
+    c.dirty = false;
   }
 
   // udpGRO (gro.go:971-1095) after its pre-checks
@@ -348,26 +370,33 @@ struct Planner {
   // its own flow's, so every flow of a call runs on its own thread.
   __device__ void run_flow(int f) {
     const bool tcp = S.cand[f] <= C_TCP6;
+    if (!tcp) {
+      for (int i = f; i != kNone; i = S.fnext[i]) S.res[i] = (uint8_t)udp_gro(i);
+      return;
+    }
     TailCache c;
     c.it = kNone;
-    bool fresh = false;  // c mirrors the flow's last item in LDS
-    for (int i = f, nx; i != kNone; i = nx) {  // the flow's packets in order (fnext links)
-      nx = S.fnext[i];
-      if (!tcp) {
-        S.res[i] = (uint8_t)udp_gro(i);
-        continue;
-      }
+    c.dirty = false;
+    bool fresh = false;  // c mirrors the flow's last item
+    uint4 R = S.rec[f];
+    for (int i = f; i != kNone;) {  // the flow's packets in order (fnext links)
+      const int nx = (int)(int16_t)(R.z >> 16);
+      const uint4 Rn = nx != kNone ? S.rec[nx] : R;  // the next record, a step ahead
       if (!fresh) {
         load_tail(c, f);
         fresh = true;
       }
-      if (tcp_append_fast(c, i)) {
+      if (tcp_append_fast(c, i, R)) {
         S.res[i] = R_COALESCED;
-        continue;
+      } else {
+        flush_tail(c);
+        S.res[i] = (uint8_t)tcp_gro(i);
+        fresh = false;  // inserts, prepends, deletes: reload from LDS
       }
-      S.res[i] = (uint8_t)tcp_gro(i);
-      fresh = false;  // inserts, prepends, deletes: reload from LDS
+      i = nx;
+      R = Rn;
     }
+    flush_tail(c);
   }
 
   // apply{TCP,UDP}Coalesce (gro.go:1364-1366) for item `it`, or -- after
@@ -693,10 +722,21 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
   }
   __syncthreads();
 
-  // ---- 3. the handleGRO loop: one thread per flow
+  // ---- 3. the handleGRO loop: one thread per flow.  First each packet's
+  // PktRec -- {seq, ipattr, gsoSize | fnext << 16, th | iph << 8 | psh << 16 |
+  // valid << 24} -- over the dead key words, so the walker fetches a packet
+  // with one LDS read and prefetches the next one while it decides this one.
+  uint4 rec = make_uint4(0, 0, 0, 0);
+  const bool live = t < n_eff && S.cand[t] != C_NOT && !S.noop[t];
+  if (live)
+    rec = make_uint4(S.seq[t], S.ipattr[t], (uint32_t)S.gso[t] | ((uint32_t)(uint16_t)S.fnext[t] << 16),
+                     (uint32_t)S.th[t] | ((uint32_t)S.iph[t] << 8) | ((uint32_t)S.psh[t] << 16) |
+                         ((uint32_t)S.valid[t] << 24));
+  if (live) S.rec[t] = rec;  // step 2's key-word reads ended at the barrier above
+  __syncthreads();
   const bool raw = n_eff < n;  // "invalid offset": coalescing happened, apply* did not
   Planner P{S, arena, offset};
-  if (t < n_eff && S.cand[t] != C_NOT && !S.noop[t] && S.flow[t] == t) P.run_flow(t);
+  if (live && S.flow[t] == t) P.run_flow(t);
   __syncthreads();
   // toWrite in packet order (groResultNoop and groResultTableInsert,
   // gro.go:1349-1362); NOOP buffers get an empty virtioNetHdr (:1350-1358)

@@ -17,25 +17,69 @@ import time
 
 import numpy as np
 
-from . import shard, synth
+from . import shard, synth, traffic
 
 OFFSET = 16
 CAP = 65535 + OFFSET
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, MI355X_MICROARCH.md
 
 
+def flow_segments(dev, n_pkts: int, mss: int = 1448, seed: int = synth.SEED, tcp_flags: int = 0x10):
+    """n_pkts in-order TCP/IPv4 segments of ONE flow (any count: the flow is cut
+    into super-packets of at most 45 segments that share the IP/TCP header and
+    continue its sequence numbers), each made by the product's GSO split."""
+    out, seq_step, first = [], 0, None
+    while len(out) < n_pkts:
+        k = min(45, n_pkts - len(out))
+        vp = bytearray(synth.make_super_packet(40 + k * mss, mss, seed=seed + 7919 * len(out), tcp_flags=tcp_flags))
+        if first is None:
+            first = bytes(vp[10:50])
+        else:  # the flow's header, sequence number continued
+            vp[10:50] = first
+            vp[12:14] = (40 + k * mss).to_bytes(2, "big")
+            seq = (int.from_bytes(first[24:28], "big") + seq_step) & 0xFFFFFFFF
+            vp[34:38] = seq.to_bytes(4, "big")
+        bufs = [np.zeros(mss + 200, np.uint8) for _ in range(k + 2)]
+        sizes = [0] * len(bufs)
+        n, err = dev.handle_virtio_read(np.frombuffer(vp, np.uint8).copy(), bufs, sizes, OFFSET)
+        assert err is None and n == k, (n, err)
+        out += [bufs[i][OFFSET: OFFSET + sizes[i]].tobytes() for i in range(n)]
+        seq_step += k * mss
+    return out
+
+
 def make_batch(dev, flows: int = 4, per_flow: int = 32, mss: int = 1448, seed: int = synth.SEED):
     """128 segmented TCP/IPv4 packets, produced by the product's GSO split of
     one super-packet per flow (flows interleaved round-robin, in order per flow)."""
-    segs = []
-    for f in range(flows):
-        vp = synth.make_super_packet(40 + per_flow * mss, mss, seed=seed + f, tcp_flags=0x10)
-        bufs = [np.zeros(mss + 200, np.uint8) for _ in range(per_flow + 2)]
-        sizes = [0] * len(bufs)
-        n, err = dev.handle_virtio_read(np.frombuffer(bytearray(vp), np.uint8).copy(), bufs, sizes, OFFSET)
-        assert err is None and n == per_flow, (n, err)
-        segs.append([bufs[i][OFFSET: OFFSET + sizes[i]].tobytes() for i in range(n)])
+    segs = [flow_segments(dev, per_flow, mss, seed + f) for f in range(flows)]
     return [segs[f][k] for k in range(per_flow) for f in range(flows)]
+
+
+# Write-call shapes of the gro_device bench (VERDICT r2: the per-flow walk is
+# one thread per flow, so one long flow or prepend chains are its worst case).
+CALL_SHAPES = {
+    "4x32": "4 TCP/IPv4 flows x 32 in-order 1448-B MSS segments, interleaved (bulk transfer)",
+    "1x128": "one TCP/IPv4 flow of 128 in-order 1448-B segments (one walker does all 128 steps)",
+    "4x32rev": "4 flows x 32 segments, each flow in reverse order: every packet prepends to its item (gro.go:648-697)",
+    "1x128rev": "one flow of 128 segments in reverse order (a 128-step prepend chain)",
+    "shuffled": "4 flows x 32 segments in a seeded random order (appends, prepends and new items mixed)",
+}
+
+
+def shape_batch(dev, shape: str):
+    if shape == "4x32":
+        return make_batch(dev)
+    if shape in ("1x128", "1x128rev"):
+        f = flow_segments(dev, 128)
+        return f[::-1] if shape.endswith("rev") else f
+    if shape == "4x32rev":
+        segs = [flow_segments(dev, 32, seed=synth.SEED + f)[::-1] for f in range(4)]
+        return [segs[f][k] for k in range(32) for f in range(4)]
+    if shape == "shuffled":
+        pk = make_batch(dev)
+        order = np.random.default_rng(synth.SEED).permutation(len(pk))
+        return [pk[i] for i in order]
+    raise ValueError(shape)
 
 
 class Batch:
@@ -310,7 +354,8 @@ def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int =
     from .tun import GRO_BUF_DTYPE, GRO_CALL_DTYPE, GRO_CAN_UDP
 
     calls = int(os.environ.get("WGCS_GRO_CALLS", calls))
-    pkts = make_batch(dev)
+    shape = getattr(args, "gro_shape", "4x32")
+    pkts = shape_batch(dev, shape)
     n = len(pkts)
     N = calls * n
     stride = (CAP + 15) // 16 * 16
@@ -354,9 +399,20 @@ def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int =
     restore()
     launch(0)
     torch.cuda.synchronize()
-    assert bool((st[0] == 0).all()) and bool((nw[0] == 4).all()), (st[0][:4], nw[0][:4])
-    heads = d_bufs[0].cpu().numpy().view(GRO_BUF_DTYPE)["len"].reshape(calls, n)[:, :4]
-    assert (heads == OFFSET + 40 + 32 * 1448).all(), heads[0]
+    # every call is the same batch: the same status and write count everywhere
+    # (the per-byte parity of each shape is tests/test_gpu_gro_batch.py's)
+    assert bool((st[0] == 0).all()) and bool((nw[0] == nw[0][0]).all()), (st[0][:4], nw[0][:4])
+    n_write = int(nw[0][0].item())
+    # bytes the reference's appends and prepend copies move (gro.go:648-697):
+    # every copy grows len(bufs[j]) of its destination, and lengths only grow,
+    # so the copied volume is the growth of all slice lengths (a prepend chain
+    # copies its whole item at every step: quadratic in the chain length)
+    lens0 = d_bufs0.cpu().numpy().view(GRO_BUF_DTYPE)["len"].astype(np.int64)
+    lens1 = d_bufs[0].cpu().numpy().view(GRO_BUF_DTYPE)["len"].astype(np.int64)
+    copied = int(lens1.sum() - lens0.sum())
+    if shape == "4x32":
+        heads = d_bufs[0].cpu().numpy().view(GRO_BUF_DTYPE)["len"].reshape(calls, n)[:, :4]
+        assert n_write == 4 and (heads == OFFSET + 40 + 32 * 1448).all(), heads[0]
     for _ in range(max(0, args.warmup - 1)):
         restore()
         for r in range(R):
@@ -390,8 +446,8 @@ def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int =
     payload = sum(len(p) for p in pkts) * calls
     # algorithmic bytes per launch: every candidate byte read once (checksumValid),
     # every appended payload read and written once, the rewritten headers
-    appended = sum(len(p) - 40 for k, p in enumerate(pkts) if k >= 4) * calls
-    algo = payload + 2 * appended + 4 * calls * (10 + 40)
+    # every copied byte read and written once (`copied`, above)
+    algo = payload + 2 * copied + n_write * calls * (10 + 40)
     achieved = algo / (kern_ms * 1e-3) / 1e9
     result = {
         "metric": "device-resident Tun.Write handleGRO packets/s (batch of Write calls in HBM)",
@@ -407,8 +463,10 @@ def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int =
         "dtype": "u8",
         "data": "synthetic",
         "config": {
-            "workload": f"{calls} Tun.Write calls per launch, each the 128-packet batch (4 TCP/IPv4 flows x 32 x "
-                        "1448-B MSS) coalesced to 4 packets, buffers of cap 65,551 B in HBM, in place",
+            "workload": f"{calls} Tun.Write calls per launch, each 128 packets: {CALL_SHAPES[shape]}; coalesced to "
+                        f"{n_write} packets, buffers of cap 65,551 B in HBM, in place",
+            "call_shape": shape,
+            "writes_per_call": n_write,
             "packets_per_step": N,
             "payload_bytes_per_step": payload,
             "rotated_copies": R,
@@ -422,14 +480,16 @@ def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int =
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": traffic.per_launch("gro_batch_kernel", algo),
             "kernel": "gro_batch_kernel",
             "kernel_ms": round(kern_ms, 5),
             "kernel_ms_is": "GPU time per launch (HIP events around each burst of launches"
                             + (f"; {S} streams, consecutive launches overlap)" if S > 1 else ")"),
             "algorithmic_bytes_per_launch": algo,
-            "note": "one thread per call runs handleGRO's flow-table loop; the launch is bound by that "
-                    "sequential planner, not by HBM",
+            "copied_bytes_per_launch": copied,
+            "note": "algorithmic bytes: every candidate byte read once (checksumValid) + every byte the "
+                    "reference's append / prepend copies move, read and written (the growth of all slice "
+                    "lengths) + the rewritten headers; one thread per flow runs handleGRO's flow-table walk",
         },
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
