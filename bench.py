@@ -221,8 +221,8 @@ def main():
         t0 = time.perf_counter()
         dev.checksum_batches(mode, bl, streams[:ns], e0 if use_events else None, e1 if use_events else None)
         torch.cuda.synchronize()
+        el = time.perf_counter() - t0  # the closing barrier is not timed: max over ranks covers skew
         barrier()
-        el = time.perf_counter() - t0
         return el, (e0.elapsed_time(e1) / K if use_events else None)
 
     # The one-stream reference (untimed for `value`) runs first, before the
@@ -412,8 +412,9 @@ def end_to_end(torch, dev, arena_np, pkts_np, mode, barrier, dist, red_dev, worl
         for _ in range(iters):
             fn()
         torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / iters
         barrier()
-        return shard.max_over_ranks((time.perf_counter() - t0) / iters, dist, device=red_dev)
+        return shard.max_over_ranks(dt, dist, device=red_dev)
 
     dt_pipe = timed(pipelined)
     dt_ser = timed(serialized)

@@ -273,8 +273,9 @@ def run_staged(args, torch, dev, dist, rank, world, local, barrier, calls_per_sl
         step()
     while inflight:
         settle(inflight.pop(0))
+    dt = time.perf_counter() - t0
     barrier()
-    dt = shard.max_over_ranks(time.perf_counter() - t0, dist)
+    dt = shard.max_over_ranks(dt, dist)
     per = dt / args.steps
     ws.close()
     if pool is not None:

@@ -65,8 +65,9 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
             streams[0].wait_event(j)
         e1.record(streams[0])
         torch.cuda.synchronize()
+        el = time.perf_counter() - t0
         barrier()
-        return time.perf_counter() - t0, e0.elapsed_time(e1) / K
+        return el, e0.elapsed_time(e1) / K
 
     if args.warmup > 0:  # the W warmup steps go through the same bracket as the timed ones
         timed(args.warmup, 0, S)

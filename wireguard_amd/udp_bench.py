@@ -67,8 +67,9 @@ def _time_steps(torch, streams, step, steps, warmup, barrier):
             streams[0].wait_event(j)
         e1.record(streams[0])
         torch.cuda.synchronize()
+        el = time.perf_counter() - t0
         barrier()
-        return time.perf_counter() - t0, e0.elapsed_time(e1) / K
+        return el, e0.elapsed_time(e1) / K
 
     el, ms = timed(steps, warmup, S)
     iso = timed(max(steps, 10), warmup + steps, 1)[1] if S > 1 else None
