@@ -133,6 +133,8 @@ def load() -> C.CDLL:
                                  C.POINTER(sz)], i32),
     }
     for name, (args, res) in sig.items():
+        if os.environ.get("WGCS_LIB") and not hasattr(L, name):
+            continue  # an A/B build of an older revision (scripts/probe_lib_bench.sh)
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res

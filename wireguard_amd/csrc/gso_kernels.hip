@@ -968,8 +968,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
       status[jb] = many ? WGCS_ERR_TOO_MANY_SEGMENTS : 0;
     }
     const int type = type_s, ipv = ipv_s, hdr_len = hdr_s, gso = gso_s, cs = cs_s, co = co_s, plen = plen_s;
+    // job-constant header sums from this row's own header chunks (header_fast's
+    // values): IPv4 header without total length / id / checksum, the L4
+    // header from csumStart without checksum field, seq / UDP length and the
+    // flags byte, and the pseudo-header addresses, each as BE words
     uint32_t ip_base = 0, l4_base = 0, tflags = 0, id0 = 0, seq0 = 0;
-    bool sums = false;  // the job-constant header sums, made once, after the first payload loads are out
+    {
+      const int x0 = 16 * r;
+      const bool tcp_c = type != GSO_UDP_L4;
+      const int vlo = cs + 4, vhi = tcp_c ? cs + 8 : cs + 6;
+      const int ca = (cs + co) & 0xFFFF;
+      if (ipv == 4) {
+        const uint32_t m = byte_bits16(-x0, cs - x0) & ~byte_bits16(2 - x0, 6 - x0) & ~byte_bits16(10 - x0, 12 - x0);
+        ip_base = (uint32_t)ufl((int)bswap16(fold32_16(row16_sum_u32(add4_masked(0u, Q, m, false)))));
+      }
+      uint32_t ml4 = byte_bits16(cs - x0, hdr_len - x0) & ~byte_bits16(ca - x0, ca + 2 - x0) &
+                     ~byte_bits16(vlo - x0, vhi - x0);
+      if (tcp_c) ml4 &= ~byte_bits16(cs + 13 - x0, cs + 14 - x0);
+      const int a_lo = ipv == 4 ? 12 : 8, a_hi = ipv == 4 ? 20 : 40;
+      uint32_t s4 = add4_masked(0u, Q, ml4, false);
+      s4 = add4_masked(s4, Q, byte_bits16(a_lo - x0, a_hi - x0), (cs & 1) != 0);
+      uint32_t t4 = fold32_16(row16_sum_u32(s4));
+      if ((cs & 1) == 0) t4 = bswap16(t4);  // pairing from csumStart (packet coordinates)
+      if (tcp_c) tflags = qbyte(Q, cs + 13);
+      l4_base = (uint32_t)ufl((int)t4) + (tflags & ~0x09u);
+      if (ipv == 4) id0 = (qbyte(Q, 4) << 8) | qbyte(Q, 5);
+      if (tcp_c) seq0 = (qbyte(Q, vlo) << 24) | (qbyte(Q, vlo + 1) << 16) | (qbyte(Q, vlo + 2) << 8) | qbyte(Q, vlo + 3);
+    }
     for (int grp = (int)blockIdx.y; grp * ROWS < nseg_s; grp += (int)gridDim.y) {  // block-uniform
       const int i = grp * ROWS + wv * 4 + (lane >> 4);  // this row's segment
       if (i < nseg_s) {  // row-uniform
@@ -979,35 +1004,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
         // ---- the payload stream
         uint32_t acc = 0;
         stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen));
-        if (!sums) {
-          // job-constant header sums from this row's own header chunks (header_fast's
-          // values): IPv4 header without total length / id / checksum, the L4
-          // header from csumStart without checksum field, seq / UDP length and the
-          // flags byte, and the pseudo-header addresses, each as BE words
-          {
-            const int x0 = 16 * r;
-            const bool tcp_c = type != GSO_UDP_L4;
-            const int vlo = cs + 4, vhi = tcp_c ? cs + 8 : cs + 6;
-            const int ca = (cs + co) & 0xFFFF;
-            if (ipv == 4) {
-              const uint32_t m = byte_bits16(-x0, cs - x0) & ~byte_bits16(2 - x0, 6 - x0) & ~byte_bits16(10 - x0, 12 - x0);
-              ip_base = (uint32_t)ufl((int)bswap16(fold32_16(row16_sum_u32(add4_masked(0u, Q, m, false)))));
-            }
-            uint32_t ml4 = byte_bits16(cs - x0, hdr_len - x0) & ~byte_bits16(ca - x0, ca + 2 - x0) &
-                           ~byte_bits16(vlo - x0, vhi - x0);
-            if (tcp_c) ml4 &= ~byte_bits16(cs + 13 - x0, cs + 14 - x0);
-            const int a_lo = ipv == 4 ? 12 : 8, a_hi = ipv == 4 ? 20 : 40;
-            uint32_t s4 = add4_masked(0u, Q, ml4, false);
-            s4 = add4_masked(s4, Q, byte_bits16(a_lo - x0, a_hi - x0), (cs & 1) != 0);
-            uint32_t t4 = fold32_16(row16_sum_u32(s4));
-            if ((cs & 1) == 0) t4 = bswap16(t4);  // pairing from csumStart (packet coordinates)
-            if (tcp_c) tflags = qbyte(Q, cs + 13);
-            l4_base = (uint32_t)ufl((int)t4) + (tflags & ~0x09u);
-            if (ipv == 4) id0 = (qbyte(Q, 4) << 8) | qbyte(Q, 5);
-            if (tcp_c) seq0 = (qbyte(Q, vlo) << 24) | (qbyte(Q, vlo + 1) << 16) | (qbyte(Q, vlo + 2) << 8) | qbyte(Q, vlo + 3);
-          }
-          sums = true;
-        }
         finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
                    tflags, id0, seq0, &sizes[slot0 + (uint32_t)i]);
       }

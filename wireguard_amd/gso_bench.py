@@ -69,6 +69,14 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
         barrier()
         return el, e0.elapsed_time(e1) / K
 
+    # The one-stream reference (untimed for `value`) runs first, as in bench.py:
+    # measured after a two-stream burst the same launches read 2-3 us slower
+    # (profiles/r2_probe_iso_order.txt; cfg4: 11.7-12.3 us after, 9.8 us in a
+    # fresh process, profiles/r3_probe_gso_path.jsonl).
+    iso_ms = None
+    if S > 1:
+        timed(min(args.warmup, 5), 0, 1)
+        iso_ms = timed(max(args.steps, 20), 0, 1)[1]
     if args.warmup > 0:  # the W warmup steps go through the same bracket as the timed ones
         timed(args.warmup, 0, S)
     torch.cuda.synchronize()
@@ -81,7 +89,6 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
     bytes_per_step = bytes_in + bytes_out
     elapsed, kern_ms = timed(args.steps, args.warmup, S)
     elapsed = shard.max_over_ranks(elapsed, dist)
-    iso_ms = timed(max(args.steps, 20), args.warmup + args.steps, 1)[1] if S > 1 else None
     stream = streams[0]
     achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
     # calibration: a plain device-to-device copy of the super-packet bytes
