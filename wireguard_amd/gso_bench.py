@@ -69,10 +69,9 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
         barrier()
         return el, e0.elapsed_time(e1) / K
 
-    # The one-stream reference (untimed for `value`) runs first, as in bench.py:
-    # measured after a two-stream burst the same launches read 2-3 us slower
-    # (profiles/r2_probe_iso_order.txt; cfg4: 11.7-12.3 us after, 9.8 us in a
-    # fresh process, profiles/r3_probe_gso_path.jsonl).
+    # The one-stream reference (untimed for `value`) runs first, as in bench.py
+    # (measured after a two-stream burst, cfg2's launches read 2-3 us slower,
+    # profiles/r2_probe_iso_order.txt).
     iso_ms = None
     if S > 1:
         timed(min(args.warmup, 5), 0, 1)
