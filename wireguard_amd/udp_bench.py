@@ -46,9 +46,6 @@ def _time_steps(torch, streams, step, steps, warmup, barrier):
     returns (wall seconds, GPU ms per launch over the timed region, the same
     on one stream or None)."""
     S = len(streams)
-    for k in range(warmup):
-        step(k, S)
-    torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     joins = [torch.cuda.Event() for _ in streams[1:]]
@@ -71,8 +68,16 @@ def _time_steps(torch, streams, step, steps, warmup, barrier):
         barrier()
         return el, e0.elapsed_time(e1) / K
 
+    # the one-stream reference first (as bench.py: measured after a two-stream
+    # burst, launches read slower, profiles/r2_probe_iso_order.txt), then the W
+    # warmup steps through the same bracket as the K timed ones
+    iso = None
+    if S > 1:
+        timed(min(warmup, 5), 0, 1)
+        iso = timed(max(steps, 10), 0, 1)[1]
+    if warmup > 0:
+        timed(warmup, 0, S)
     el, ms = timed(steps, warmup, S)
-    iso = timed(max(steps, 10), warmup + steps, 1)[1] if S > 1 else None
     return el, ms, iso
 
 
