@@ -42,14 +42,19 @@ if want lines; then
   line cfg3 300 --config cfg3 --steps 100 --warmup 10 --cpu-seconds 4
   line cfg5 300 --config cfg5 --steps 50 --warmup 5 --cpu-seconds 4
   line cfg4 300 --config cfg4 --steps 100 --warmup 10 --cpu-seconds 4
+  line cfg4_64slots 300 --config cfg4 --max-segs 64 --steps 100 --warmup 10 --cpu-seconds 0 --no-e2e
   line cfg1 300 --config cfg1 --steps 200 --warmup 20 --cpu-seconds 4
   line gro 300 --config gro --steps 200 --warmup 20 --cpu-seconds 3
   line gro_staged 300 --config gro_staged --steps 30 --warmup 5 --cpu-seconds 3
   line gro_device 300 --config gro_device --steps 40 --warmup 4 --cpu-seconds 3
+  line gro_device_1x128 300 --config gro_device --gro-shape 1x128 --steps 40 --warmup 4 --cpu-seconds 0
+  line gro_device_4x32rev 300 --config gro_device --gro-shape 4x32rev --steps 20 --warmup 2 --cpu-seconds 0
   line udp_split 300 --config udp_split --steps 50 --warmup 5 --cpu-seconds 3
   line udp_coalesce 300 --config udp_coalesce --steps 50 --warmup 5 --cpu-seconds 3
 fi
 if want prof; then
+  (cd /tmp && step prof_driver 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_driver" -o run --output-format csv -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --no-e2e)
+  python3 scripts/trace_span.py "$OUT/prof_driver/run_kernel_trace.csv" checksum_batch 20 20 | sed "s/^{/{\"run\": \"prof_driver\", /" >> "$OUT/trace_span.jsonl"
   (cd /tmp && step prof_cfg2 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg2" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e)
   (cd /tmp && step prof_cfg2_1s 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg2_1s" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e --streams 1)
   (cd /tmp && step prof_cfg4 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg4" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 100 --warmup 10 --cpu-seconds 0 --no-e2e)
