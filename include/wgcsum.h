@@ -161,8 +161,9 @@ int wgcs_checksum_batch(wgcs_ctx *ctx, int mode, unsigned flags, uint8_t *d_aren
  * context's stream), in order, with wgcs_checksum_batch's semantics.  Optional
  * bracket events (hipEvent_t as void*, created by the caller): ev_begin is
  * recorded on streams[0] before the first launch and the other streams wait on
- * it before their first; after the last launch every other stream is joined
- * to streams[0] and ev_end is recorded there, so the pair spans every launch.
+ * it before their first; after the last launch every other stream that got a
+ * batch is joined to streams[0] and ev_end is recorded there, so the pair
+ * spans every launch.
  * All arguments are checked before anything is enqueued. */
 typedef struct wgcs_batch {
   uint8_t *arena;

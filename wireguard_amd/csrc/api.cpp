@@ -285,7 +285,10 @@ int wgcs_checksum_batches(wgcs_ctx* ctx, int mode, unsigned flags, const wgcs_ba
     if (e != hipSuccess) return hip_fail(ctx, e, "checksum_batches launch");
   }
   if (ev_end) {
-    for (uint32_t j = 1; j < ns; ++j) {
+    // join only the streams that received a batch: a stream without one may
+    // hold unrelated work that must not land inside the bracket
+    const uint32_t used = n_batches < ns ? n_batches : ns;
+    for (uint32_t j = 1; j < used; ++j) {
       if (st[j] == st[0]) continue;
       if ((e = hipEventRecord(ctx->join_ev[j], st[j])) != hipSuccess ||
           (e = hipStreamWaitEvent(st[0], ctx->join_ev[j], 0)) != hipSuccess)
