@@ -15,6 +15,8 @@
  *                             + gsoSplit's per-segment L4 sum      tun/gro.go:1469-1488
  *                             + gsoNoneChecksum()                 tun/gro.go:1497-1517
  *                             + IPv4 header checksum sites        tun/gro.go:1134-1138,1217-1221,1434-1436
+ *   wgcs_checksum_batches     many such batches enqueued by one call over several streams
+ *                             (consecutive Tun.Read / Tun.Write batches, tun/tun.go:477-508, :654-700)
  *   wgcs_checksum             checksum(b, initial)                tun/checksum.go:152-167
  *   wgcs_checksum_valid       checksumValid(pkt, iphLen, proto, isV6)  tun/gro.go:554-612
  *   wgcs_gso_none_checksum    gsoNoneChecksum(readBuf, start, off)     tun/gro.go:1497-1517
