@@ -587,15 +587,15 @@ __device__ __forceinline__ void stream_row(const uint8_t* rb, int i, int gso, in
 // Byte `pos` (wave-uniform, < 16 * 16) of the header chunks in packet
 // coordinates (lane r of each row holds readBuf[16r, 16r + 16)), from the
 // wave's first row.
-__device__ __forceinline__ uint32_t qbyte(const uint4& Q, int pos) {
-  const int l = pos >> 4;
-  const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)Q.x, l), y = (uint32_t)__builtin_amdgcn_readlane((int)Q.y, l);
-  const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)Q.z, l), w = (uint32_t)__builtin_amdgcn_readlane((int)Q.w, l);
-  const int c = (pos >> 2) & 3;
-  const uint32_t d = c == 0 ? x : (c == 1 ? y : (c == 2 ? z : w));
-  return (d >> (8 * (pos & 3))) & 0xFFu;
+__device__ __forceinline__ uint32_t qdw(const uint4& Q, int dw) {  // dword dw (wave-uniform, < 64)
+  return (uint32_t)__builtin_amdgcn_readlane((int)dword_at(Q, dw & 3), dw >> 2);
 }
-
+__device__ __forceinline__ uint32_t qbyte(const uint4& Q, int pos) { return (qdw(Q, pos >> 2) >> (8 * (pos & 3))) & 0xFFu; }
+// Bytes [pos, pos + 4) as a little-endian u32 (two readlanes).
+__device__ __forceinline__ uint32_t qle32(const uint4& Q, int pos) {
+  const uint64_t w = ((uint64_t)qdw(Q, (pos >> 2) + 1) << 32) | qdw(Q, pos >> 2);
+  return (uint32_t)(w >> (8 * (pos & 3)));
+}
 // The decoded path's decoder (wave 0 of the block): handleVirtioRead's /
 // gsoSplit's checks and geometry (decode_job) and the job-constant header
 // sums (header_fast), published in `ji`; count / status of the job.  Kept out
@@ -864,6 +864,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
                                                        uint32_t room, int32_t* __restrict__ sizes,
                                                        int32_t* __restrict__ count, int32_t* __restrict__ status) {
   constexpr int ROWS = 16;
+#ifdef WGCS_GSO_STAMPS  // timing-only build (scripts/probe_gso_stamps.py): s_memrealtime per wave phase
+  uint64_t stp[5] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0};
+#endif
   const int lane = threadIdx.x & 63;
   const int r = lane & 15;
   const int wv = threadIdx.x >> 6;
@@ -925,8 +928,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   const bool clean_s = ok_s && hdr_s < plen_s && cs_s >= (ipv_s == 4 ? 20 : 40) && ca_s + 2 <= hdr_s &&
                        hdr_s <= kMaxHdrLen && (raw || !tcp_s || (hdr_s - cs_s >= 20 && hdr_s - cs_s <= 60)) &&
                        fast_header(cs_s, hdr_s, ca_s, tcp_s) && (uint32_t)pkt0_s <= room;
-  const int nfull_s = clean_s ? (plen_s - hdr_s + gso_s - 1) / gso_s : 0;
-  const int nseg_s = min(nfull_s, (int)max_segs);
+  // Row i of a clean job holds a segment iff i < max_segs and hdrLen + i *
+  // gsoSize < len(readBuf) (i < ceil((plen - hdrLen) / gsoSize)): a multiply,
+  // no division, on the clean path.
+  auto has_seg = [&](int i) { return i < (int)max_segs && hdr_s + (int64_t)i * gso_s < plen_s; };
   // Segment groups: this block takes groups blockIdx.y, + gridDim.y, ... of
   // the job's ceil(max_segs / 16).  The grid has only a few blocks per job
   // (callers size bufs for the largest read, conn.IdealBatchSize = 128 slots,
@@ -935,19 +940,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   // hdrLen >= csumStart + 20 (TCP, tun.go:608-613) or = csumStart + 8 (UDP) or
   // the virtio value (raw jobs) bounds the segment count from above.  Group 0
   // always runs: it writes count / status and the GSO_NONE packet.
+  // Groups that may hold a segment: gbound = max(1, min(ngroups, ceil(nbound /
+  // 16))) with nbound = ceil((plen - hmin) / gsoSize); group y < gbound iff y
+  // == 0 or (y < ngroups and 16 y gsoSize < plen - hmin).
   const int ngroups = (int)((max_segs + ROWS - 1) / ROWS);
-  int gbound = ngroups;  // groups that may hold a segment
-  if (jlen >= 14) {
-    const int hmin = raw ? (int)hl : (tcp_s ? cs_s + 20 : cs_s + 8);
-    const bool split_type = ok_s && cs_s + 60 <= 0xFFFF;
-    if (!raw && t1 == GSO_NONE) {
-      gbound = 1;
-    } else if (split_type) {
-      const int nbound = plen_s > hmin ? (plen_s - hmin + gso_s - 1) / gso_s : 0;
-      gbound = max(1, min(ngroups, (nbound + ROWS - 1) / ROWS));
-    }
-  }
-  if ((int)blockIdx.y >= gbound) return;
+  const int hmin = raw ? (int)hl : (tcp_s ? cs_s + 20 : cs_s + 8);
+  const bool split_type = jlen >= 14 && ok_s && cs_s + 60 <= 0xFFFF;
+  const bool gso_none = jlen >= 14 && !raw && t1 == GSO_NONE;
+  auto group_live = [&](int y) {
+    if (y == 0) return true;
+    if (gso_none || y >= ngroups) return false;
+    return !split_type || (plen_s > hmin && hmin + (int64_t)y * ROWS * gso_s < plen_s);
+  };
+  if (!group_live((int)blockIdx.y)) return;
 
   uint4 Q = funnel(H0, H1, hph);  // readBuf[16r, 16r + 16) (bytes below hdrLen)
   // the TCP data offset decides hdrLen (tun.go:601-614): block-uniform verdict
@@ -963,6 +968,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   // the virtio header).  readfirstlane makes the branch provably uniform.
   if (ufl(clean ? 1 : 0)) {
     if (blockIdx.y == 0 && threadIdx.x == 0) {  // the checks can only end in the segment count here
+      const int nfull_s = (plen_s - hdr_s + gso_s - 1) / gso_s;
       const bool many = nfull_s > (int)max_segs;
       count[jb] = many ? (int)max_segs - 1 : nfull_s;
       status[jb] = many ? WGCS_ERR_TOO_MANY_SEGMENTS : 0;
@@ -992,24 +998,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
       if ((cs & 1) == 0) t4 = bswap16(t4);  // pairing from csumStart (packet coordinates)
       if (tcp_c) tflags = qbyte(Q, cs + 13);
       l4_base = (uint32_t)ufl((int)t4) + (tflags & ~0x09u);
-      if (ipv == 4) id0 = (qbyte(Q, 4) << 8) | qbyte(Q, 5);
-      if (tcp_c) seq0 = (qbyte(Q, vlo) << 24) | (qbyte(Q, vlo + 1) << 16) | (qbyte(Q, vlo + 2) << 8) | qbyte(Q, vlo + 3);
+      if (ipv == 4) {
+        const uint32_t b45 = qdw(Q, 1);  // readBuf[4:8)
+        id0 = ((b45 & 0xFFu) << 8) | ((b45 >> 8) & 0xFFu);
+      }
+      if (tcp_c) seq0 = __builtin_bswap32(qle32(Q, vlo));
     }
-    for (int grp = (int)blockIdx.y; grp * ROWS < nseg_s; grp += (int)gridDim.y) {  // block-uniform
+#ifdef WGCS_GSO_STAMPS
+    stp[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef WGCS_GSO_HEADONLY  // timing-only build: the head (decode, verdict, job sums) and nothing else
+    if (ufl((int)(ip_base + l4_base + tflags + id0 + seq0)) == 0x7FFFFFFF) sizes[slot0] = 0;
+    return;
+#endif
+    for (int grp = (int)blockIdx.y; has_seg(grp * ROWS); grp += (int)gridDim.y) {  // block-uniform
       const int i = grp * ROWS + wv * 4 + (lane >> 4);  // this row's segment
-      if (i < nseg_s) {  // row-uniform
+      if (has_seg(i)) {  // row-uniform
         uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
         const int dalign = (int)((uintptr_t)dst & 15u);
         uint8_t* dbase = dst - dalign;
         // ---- the payload stream
         uint32_t acc = 0;
         stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen));
+#ifdef WGCS_GSO_STAMPS
+        stp[2] = __builtin_amdgcn_s_memrealtime();
+#endif
         finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
                    tflags, id0, seq0, &sizes[slot0 + (uint32_t)i]);
+#ifdef WGCS_GSO_STAMPS
+        stp[3] = __builtin_amdgcn_s_memrealtime();
+#endif
       }
     }
+#ifdef WGCS_GSO_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stp[4] = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && max_segs >= 128) {
+      int32_t* sp = sizes + slot0 + 64 + (blockIdx.y * 4 + wv) * 5;
+      for (int k = 0; k < 5; ++k) sp[k] = (int32_t)(uint32_t)stp[k];
+    }
+#endif
   } else {
-    for (int grp = (int)blockIdx.y; grp < gbound; grp += (int)gridDim.y) {  // block-uniform
+    for (int grp = (int)blockIdx.y; group_live(grp); grp += (int)gridDim.y) {  // block-uniform
       const int i = grp * ROWS + wv * 4 + (lane >> 4);
       uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
       decoded_rows<U, NT>(vb, jlen, job.flags, room, max_segs, i, grp == 0, &count[jb], &status[jb],

@@ -80,13 +80,72 @@ __device__ __forceinline__ uint32_t dword_at(const uint4& v, int i) {
 // byte/short/dword/dwordx2 pieces (at most 7 stores instead of 16 bytes).
 // Each piece's value is picked by dword selects: every piece lies inside one
 // dword, or is the aligned dword pair (0,1) / (2,3).
+//
+// The two one-sided cases -- the chunk's first bytes [0, hi) (a packet's last
+// chunk) and its last bytes [lo, 16) (the chunk a packet, or its payload,
+// starts in) -- are by far the common partial chunks; each takes at most
+// four stores whose values come from fixed dwords shifted as they are
+// consumed (no per-piece dword selects).
+__device__ __forceinline__ void store_lo(uint8_t* d, const uint4& v, int hi) {  // bytes [0, hi), 0 < hi < 16
+  int p = 0;
+  uint32_t a = v.x, b = v.y;  // the dwords at p and p + 4
+  if (hi & 8) {
+    *reinterpret_cast<uint2*>(d) = make_uint2(v.x, v.y);
+    p = 8;
+    a = v.z;
+    b = v.w;
+  }
+  if (hi & 4) {
+    *reinterpret_cast<uint32_t*>(d + p) = a;
+    p += 4;
+    a = b;
+  }
+  if (hi & 2) {
+    *reinterpret_cast<uint16_t*>(d + p) = (uint16_t)a;
+    p += 2;
+    a >>= 16;
+  }
+  if (hi & 1) d[p] = (uint8_t)a;
+}
+__device__ __forceinline__ void store_hi(uint8_t* d, const uint4& v, int lo) {  // bytes [lo, 16), 0 < lo < 16
+  const int n = 16 - lo;
+  int e = 16;                 // end of the bytes still to store
+  uint32_t a = v.w, b = v.z;  // the dwords ending at e and at e - 4
+  if (n & 8) {
+    *reinterpret_cast<uint2*>(d + 8) = make_uint2(v.z, v.w);
+    e = 8;
+    a = v.y;
+    b = v.x;
+  }
+  if (n & 4) {
+    *reinterpret_cast<uint32_t*>(d + e - 4) = a;
+    e -= 4;
+    a = b;
+  }
+  if (n & 2) {
+    *reinterpret_cast<uint16_t*>(d + e - 2) = (uint16_t)(a >> 16);
+    e -= 2;
+    a <<= 16;
+  }
+  if (n & 1) d[e - 1] = (uint8_t)(a >> 24);
+}
+
 __device__ __forceinline__ void store_chunk(uint8_t* dchunk, const uint4& v, int x0, int pkt_len) {
-  if (x0 >= 0 && x0 + 16 <= pkt_len) {
+  const int lo = -x0, hi = pkt_len - x0;  // the chunk's bytes [lo, hi) are stored
+  if (lo <= 0 && hi >= 16) {
     *reinterpret_cast<uint4*>(dchunk) = v;
     return;
   }
-  int p = max(-x0, 0);
-  const int hi = min(pkt_len - x0, 16);
+  if (lo <= 0) {
+    if (hi > 0) store_lo(dchunk, v, hi);
+    return;
+  }
+  if (hi >= 16) {
+    if (lo < 16) store_hi(dchunk, v, lo);
+    return;
+  }
+  // both ends inside the chunk (a packet shorter than 16 bytes)
+  int p = lo;
   if (p >= hi) return;
   auto b8 = [&](int q) { return (uint8_t)(dword_at(v, q >> 2) >> (8 * (q & 3))); };
   auto b16 = [&](int q) { return (uint16_t)(dword_at(v, q >> 2) >> (8 * (q & 2))); };  // q even
