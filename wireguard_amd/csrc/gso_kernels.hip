@@ -884,16 +884,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
     obase = outpos[jb].base;
     opitch = outpos[jb].pitch;
   }
-  // ---- header chunks in packet coordinates (lane r of each row: the 16-byte
-  // aligned chunks r and r + 1 from the one holding readBuf[0]), issued first:
-  // they need only the descriptor.  Raw buffer loads over the job's bytes:
-  // chunks past the job read as zeros.
-  const int hph = (int)((uintptr_t)rb & 15u);
+  // ---- header chunks in packet coordinates (lane r of each row: the
+  // dword-aligned 16-byte window r from the dword holding readBuf[0]; shifted
+  // to readBuf[16r, 16r + 16) with the next lane's first dword below), issued
+  // first: they need only the descriptor.  A raw buffer load over the job's
+  // bytes: windows past the job read as zeros.  Lane 15's last bytes
+  // (readBuf[253..255]) come from the wrong lane; every use of the chunks is
+  // below hdrLen <= 240.
+  const int hph = (int)((uintptr_t)rb & 3u);
   const uint8_t* hbase = rb - hph;
   const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t*>(hbase), (short)0, (int)(jlen + 3u) - (int)(hbase - vb), 0x00020000);
-  uint4 H0 = bld16<false>(hrs, 16 * r);
-  uint4 H1 = bld16<false>(hrs, 16 * r + 16);
+  const uint4 H0 = bld16<false>(hrs, 16 * r);
 
   // ---- virtio header + the IP version byte: 16 bytes from the dword below
   // vb, one scalar load (readable: jlen >= 14 and the arena contract)
@@ -954,7 +956,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   };
   if (!group_live((int)blockIdx.y)) return;
 
-  uint4 Q = funnel(H0, H1, hph);  // readBuf[16r, 16r + 16) (bytes below hdrLen)
+  uint4 Q;  // readBuf[16r, 16r + 16) (bytes below hdrLen)
+  {
+    const uint32_t nx = row_next(H0.x);
+    Q = make_uint4(__builtin_amdgcn_alignbyte(H0.y, H0.x, hph), __builtin_amdgcn_alignbyte(H0.z, H0.y, hph),
+                   __builtin_amdgcn_alignbyte(H0.w, H0.z, hph), __builtin_amdgcn_alignbyte(nx, H0.w, hph));
+  }
   // the TCP data offset decides hdrLen (tun.go:601-614): block-uniform verdict
   bool clean = clean_s;
   if (clean && tcp_s && !raw) {
