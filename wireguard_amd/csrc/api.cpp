@@ -129,7 +129,7 @@ int wgcs_init(int device, wgcs_ctx** out) {
   const char* unr = getenv("WGCS_UNROLL");
   if (unr && atoi(unr) > 0) ctx->tune.unroll = atoi(unr);
   const char* lpp = getenv("WGCS_LANES_PER_PKT");
-  if (lpp && (atoi(lpp) == 64 || atoi(lpp) == 32)) ctx->tune.lanes_per_pkt = atoi(lpp);
+  if (lpp && (atoi(lpp) == 64 || atoi(lpp) == 32 || atoi(lpp) == 16)) ctx->tune.lanes_per_pkt = atoi(lpp);
   const char* nt = getenv("WGCS_NT");
   if (nt) ctx->tune.nt = atoi(nt) ? 1 : 0;
   const char* xc = getenv("WGCS_XCD");
