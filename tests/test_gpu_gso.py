@@ -375,3 +375,18 @@ def test_empty_bufs_gso_none(dev):
     pkt = synth.make_super_packet(1500, 1460, seed=42)[10:]
     n, err = dev.handle_virtio_read(bytes(10) + pkt, [], [], 16)
     assert err is not None and err.code == -13 and n == 0
+
+
+def test_batch_rejects_huge_max_segs(dev):
+    """len(bufs) is a Go int: wgcs_gso_split_batch refuses max_segs >= 2^31
+    (INVALID_ARG, nothing launched) instead of letting the kernel's int
+    segment bounds wrap."""
+    import torch
+
+    from wireguard_amd import WgcsError
+
+    small = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    i32 = torch.zeros(4, dtype=torch.int32, device="cuda")
+    with pytest.raises(WgcsError) as ei:
+        dev.gso_split_batch(small, small, 1, small, 16, 0, 1 << 31, i32, i32, i32)
+    assert ei.value.code == -1  # WGCS_ERR_INVALID_ARG

@@ -141,6 +141,7 @@ int wgcs_gso_split_batch(wgcs_ctx* ctx, const uint8_t* d_arena, const wgcs_gso_j
   hipSetDevice(ctx->device);
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   if ((uint64_t)n_jobs * max_segs > 0xFFFFFFFFull) return set_err(ctx, WGCS_ERR_INVALID_ARG, "n_jobs*max_segs >= 2^32");
+  if (max_segs > 0x7FFFFFFFu) return set_err(ctx, WGCS_ERR_INVALID_ARG, "max_segs >= 2^31 (len(bufs) is a Go int)");
   hipError_t e = launch_gso_split_batch(d_arena, d_jobs, n_jobs, d_out, out_stride, offset, max_segs, d_sizes, d_count,
                                         d_status, s);
   return e == hipSuccess ? WGCS_OK : hip_fail(ctx, e, "gso_split_batch launch");
