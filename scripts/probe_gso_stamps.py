@@ -46,7 +46,7 @@ arena = np.frombuffer(b"".join(pkts) + bytes(64), dtype=np.uint8).copy()
 jobs = np.zeros(n_jobs, GSO_JOB_DTYPE)
 jobs["off"] = np.arange(n_jobs, dtype=np.uint64) * np.uint64(jlen)
 jobs["len"] = jlen
-R = 8
+R = int(os.environ.get("PROBE_R", "8"))  # rotated arena / output copies
 d_arena = [torch.from_numpy(arena).cuda() for _ in range(R)]
 d_jobs = torch.from_numpy(jobs.view(np.uint8)).cuda()
 d_out = [torch.empty(n_jobs * max_segs * stride, dtype=torch.uint8, device="cuda") for _ in range(R)]
