@@ -8,8 +8,9 @@
 // Mapping (gso_rows_kernel): one 16-lane DPP row per OUTPUT segment (slot =
 // job * max_segs + i), 16 segments per 256-thread block, grid = (job,
 // segment group).  For the common ("clean") job every wave derives the split
-// geometry from the virtio header and the header chunks it loads (one scalar
-// load + two 16-byte loads per lane), issues its payload loads (dword-aligned
+// geometry from the virtio header and the header chunks it loads (one
+// 16-byte load of the virtio header + one dword-aligned 16-byte window per
+// lane), issues its payload loads (dword-aligned
 // 16-byte windows, U per lane in flight) and, with no decode step and no
 // barrier,
 //   1. shifts each window to the destination's byte phase (alignbyte with the
@@ -651,7 +652,7 @@ __device__ __noinline__ void decode_publish(const uint8_t* vb, uint32_t jlen, ui
 // segments of one job; grid = (job, segment group).
 //
 // Clean jobs (the common case) need no decode step and no barrier.  Every
-// wave reads the virtio header (one scalar load) and derives the split
+// wave reads the virtio header (one wave-uniform load) and derives the split
 // geometry; when that geometry takes the row-streaming path and its first
 // segment fits the caller's room, handleVirtioRead's and gsoSplit's checks
 // (tun/tun.go:557-631, gro.go:1387-1410) can fail only through the TCP data
@@ -898,7 +899,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   const uint4 H0 = bld16<false>(hrs, 16 * r);
 
   // ---- virtio header + the IP version byte: 16 bytes from the dword below
-  // vb, one scalar load (readable: jlen >= 14 and the arena contract)
+  // vb, one wave-uniform load (readable: jlen >= 14 and the arena contract)
   const bool raw = (job.flags & WGCS_GSO_JOB_RAW) != 0;
   const int plen_s = jlen > 10 ? (int)jlen - 10 : 0;
   uint32_t t1 = 0, hl = 0, g = 0, c = 0, o = 0, b0 = 0;
