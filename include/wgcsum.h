@@ -185,7 +185,9 @@ int wgcs_checksum_batches(wgcs_ctx *ctx, int mode, unsigned flags, const wgcs_ba
  * (like bufs[s][offset:]).  d_sizes[slot] = packet size; d_count[j] = the
  * return value n (>= 0) and d_status[j] = 0 or a WGCS_ERR_* code, with the
  * reference's ErrTooManySegments semantics (n = max_segs-1, gro.go:1409-1410).
- * Includes handleVirtioRead's GSO validation (tun/tun.go:557-631). */
+ * Includes handleVirtioRead's GSO validation (tun/tun.go:557-631).
+ * INVALID_ARG for max_segs == 0, max_segs >= 2^31 (len(bufs) is a Go int) or
+ * n_jobs * max_segs >= 2^32. */
 int wgcs_gso_split_batch(wgcs_ctx *ctx, const uint8_t *d_arena, const wgcs_gso_job *d_jobs,
                          uint32_t n_jobs, uint8_t *d_out, uint32_t out_stride, uint32_t offset,
                          uint32_t max_segs, int32_t *d_sizes, int32_t *d_count,
