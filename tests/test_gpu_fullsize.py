@@ -76,8 +76,9 @@ def test_checksum_batch_properties(dev, cfg):
     assert torch.equal(arena.cpu(), torch.from_numpy(arena_np))
 
 
-def test_gso_cfg4_properties(dev):
-    n_jobs, total, gso, max_segs, stride, offset = 256, 65535, 1460, 64, 1536, 16
+@pytest.mark.parametrize("max_segs", [64, 128])  # 128: len(bufs) of the reference's Read (bench.py cfg4)
+def test_gso_cfg4_properties(dev, max_segs):
+    n_jobs, total, gso, stride, offset = 256, 65535, 1460, 1536, 16
     vps = [synth.make_super_packet(total, gso, seed=synth.SEED + k) for k in range(n_jobs)]
     jlen = len(vps[0])
     arena_np = np.frombuffer(b"".join(vps), np.uint8).copy()
@@ -96,6 +97,8 @@ def test_gso_cfg4_properties(dev):
     count = d_count.cpu().numpy()
     assert (d_status.cpu().numpy() == 0).all() and (count == 45).all()
     sizes = d_sizes.cpu().numpy().reshape(n_jobs, max_segs)
+    assert (sizes[:, 45:] == 0).all()  # slots past the last segment untouched
+    assert not bool(d_out.view(n_jobs, max_segs, stride)[:, 45:, :].any().item())
 
     # every produced segment validates (checksum kernel over the split kernel's output)
     slots = [(j, i) for j in range(n_jobs) for i in range(45)]
