@@ -71,3 +71,48 @@ def test_cfg1_batch(dev):
         want = oracle.checksum_batch(mode, arena.copy(), pkts)
         assert np.array_equal(got, want), mode
     assert dev.checksum_batch_host(MODE_VALIDATE, arena, pkts).all()
+
+
+def _rccl_rank(port, q):
+    """bench.py's N > 1 bookkeeping on RCCL, one rank: init with device_id (as
+    bench.py binds one GPU per rank), barrier, the device-tensor max over
+    ranks, and the device-resident checksum path in between."""
+    import torch
+    import torch.distributed as dist
+
+    from wireguard_amd.tun import MODE_VALIDATE, Device
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    dev = Device(0)
+    arena, pkts, _ = synth.make_batch(512, 1500, kinds="tcp4")
+    d_arena = torch.from_numpy(arena).cuda()
+    d_pkts = torch.from_numpy(pkts.view(np.uint8)).cuda()
+    out = torch.zeros(len(pkts), dtype=torch.uint8, device="cuda")
+    dist.barrier()
+    dev.checksum_batch(MODE_VALIDATE, d_arena, d_pkts, len(pkts), out)
+    torch.cuda.synchronize()
+    dist.barrier()
+    m = shard.max_over_ranks(1.25, dist)  # device tensor all_reduce(MAX) on RCCL
+    ok = bool(out.all().item())
+    dev.close()
+    dist.destroy_process_group()
+    q.put((m, ok))
+
+
+def test_rccl_single_rank_bookkeeping():
+    """The RCCL calls bench.py makes at N > 1 (init_process_group("nccl",
+    device_id=...), barrier, all_reduce MAX of a cuda tensor), exercised on the
+    1-GPU box with one rank; the 8-GPU runs use the same calls with 8."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_rank, args=(_free_port(), q))
+    p.start()
+    m, ok = q.get(timeout=180)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert m == 1.25 and ok
