@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--max-segs", type=int, default=128,
                     help="cfg4: output slots per read = len(bufs) (the reference's Read passes conn.BatchSize = 128)")
     ap.add_argument("--verify", action="store_true", help="check the GPU results against the synth ground truth")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="cfg2: skip the configs[4] block (the 1M mixed batch split over the ranks, `cfg5_strong`)")
+    ap.add_argument("--no-affinity", action="store_true", help="do not bind each rank to its GPU's NUMA-local CPUs")
     ap.add_argument("--repeat", type=int, default=1,
                     help="diagnostics: time the K-step region this many times; `value` stays the FIRST region, "
                          "the others are listed under timing.repeats")
@@ -126,7 +129,7 @@ def main():
         args.streams = 1 if args.config in ("cfg1", "cfg5") else 2
     import torch  # before wireguard_amd: one HIP runtime per process
 
-    from wireguard_amd import shard, synth, traffic
+    from wireguard_amd import shard, synth
     from wireguard_amd.tun import Device, MODE_VALIDATE, MODE_L4_FILL
 
     world, rank, local = shard.dist_env()
@@ -155,6 +158,12 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    # N > 1: each rank on its GPU's NUMA-local cores before anything pins host
+    # memory (the Device's staging, the end-to-end leg), so the node's ranks
+    # do not cross sockets; one rank keeps the whole CPU share it was given
+    affinity = None
+    if world > 1 and not args.no_affinity:
+        affinity = shard.bind_numa_local(torch, local)
     dev = Device(local if world > 1 else 0)
     if args.config == "cfg4":
         from wireguard_amd import gso_bench
@@ -185,84 +194,18 @@ def main():
         arena_np, pkts_np, _ = synth.make_batch(n_cfg, flen, kinds=kinds, seed=synth.SEED + rank)
     n = len(pkts_np)
     bytes_per_step = int(pkts_np["len"].astype(np.int64).sum())
-    # Consecutive steps are independent batches (their own rotated arena and
-    # output), launched round-robin over S streams: step k+1's kernel streams
-    # while step k's drains and pays its end-of-kernel L2 writeback, which a
-    # single stream serialises (~1.7 us per boundary, MI355X_MICROARCH.md).
-    S = max(1, args.streams)
-    streams = [torch.cuda.Stream() for _ in range(S)]
-    R = args.rotate if bytes_per_step * args.rotate > (300 << 20) else max(args.rotate, (400 << 20) // bytes_per_step)
-    R = max(R, 2 * S)
-    arenas = [torch.from_numpy(arena_np).to("cuda") for _ in range(R)]
-    pkts = torch.from_numpy(pkts_np.view(np.uint8)).to("cuda")
-    outs = [torch.empty(n * 2, dtype=torch.uint8, device="cuda") for _ in range(R)]
-    torch.cuda.synchronize()
-
-    def batches(K, k0):  # steps k0 .. k0+K-1: each its own rotated arena and output
-        return dev.batch_list([(arenas[(k0 + k) % R], pkts, n, outs[(k0 + k) % R]) for k in range(K)])
-
-    # The K steps are enqueued by ONE library call (wgcs_checksum_batches: step k
-    # on stream k % S), which also records the HIP bracket events on the launch
-    # streams: e0 on stream 0 before the first launch (the others wait on it),
-    # every other stream joined to stream 0 before e1, so (e1 - e0) / K is the
-    # GPU time per launch over the timed region.  One call instead of K Python
-    # calls: the first launch leaves the host ~10 us sooner and no per-step
-    # ctypes/torch path runs inside the region.
     use_events = not args.no_event_timing
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(streams[0])  # torch creates the HIP events on their first record
-    e1.record(streams[0])
-
-    def timed(K, k0, ns):
-        bl = batches(K, k0)  # the step list (pointers only) is built before the clock starts
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        dev.checksum_batches(mode, bl, streams[:ns], e0 if use_events else None, e1 if use_events else None)
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0  # the closing barrier is not timed: max over ranks covers skew
-        barrier()
-        return el, (e0.elapsed_time(e1) / K if use_events else None)
-
-    # The one-stream reference (untimed for `value`) runs first, before the
-    # timed region's own W warmup steps: measured after a two-stream burst, the
-    # same launches read ~2-3 us slower per launch than in a one-stream
-    # process (profiles/r2_probe_iso_order.txt).  Then W warmup steps and
-    # exactly K timed steps, as the bench contract has it.
-    iso_first = os.environ.get("WGCS_ISO_FIRST", "1") == "1"
-    iso_ms = None
-    if use_events and S > 1 and iso_first:
-        dev.checksum_batches(mode, batches(min(args.warmup, 5), 0), streams[:1])
-        _, iso_ms = timed(max(args.steps, 20), 0, 1)
-    # W warmup steps, enqueued exactly as the timed steps are (one call, the
-    # same streams, the same bracket events): the first cross-stream wait and
-    # join on a stream costs ~40 us once per process (profiles/r3_probe_first_region.txt)
-    if args.warmup > 0:
-        dev.checksum_batches(mode, batches(args.warmup, 0), streams, e0 if use_events else None,
-                             e1 if use_events else None)
-    torch.cuda.synchronize()
-    if args.verify:
-        if mode == MODE_VALIDATE:
-            assert bool(outs[0][:n].all().item()), "VALIDATE: synthetic frames must all be valid"
-        else:  # L4 fill of a valid frame reproduces the stored checksum field
-            got = outs[0].cpu().numpy().view(np.uint16)[:n]
-            a = arena_np[: n * flen].reshape(n, flen)
-            cs = pkts_np["csum_start"].astype(np.int64) + pkts_np["csum_offset"]
-            want = (a[np.arange(n), cs].astype(np.uint16) << 8) | a[np.arange(n), cs + 1]
-            assert np.array_equal(got, want), "L4_FILL mismatch vs stored checksums"
-
-    local_elapsed, kern_ms = timed(args.steps, args.warmup, S)
-    repeats = [timed(args.steps, args.warmup + r * args.steps, S) for r in range(1, args.repeat)]
+    leg = checksum_leg(torch, dev, arena_np, pkts_np, mode, args.steps, args.warmup, args.streams, args.rotate,
+                       barrier, use_events, repeat=args.repeat, verify=args.verify)
+    local_elapsed, kern_ms, iso_ms, S, R = leg["elapsed"], leg["kern_ms"], leg["iso_ms"], leg["streams"], leg["R"]
     elapsed = shard.max_over_ranks(local_elapsed, dist, device=red_dev)
-    if use_events and S > 1 and not iso_first:  # reference: the same launches one at a time on one stream (untimed for `value`)
-        _, iso_ms = timed(max(args.steps, 20), args.warmup + args.steps, 1)
+    kern_all = shard.gather_floats(kern_ms if kern_ms is not None else -1.0, dist, device=red_dev)
 
     total_bytes = bytes_per_step * args.steps * world  # every rank processed bytes_per_step per step
     if scaling == "strong":
         total_bytes = int(n_cfg) * flen * args.steps
     value = total_bytes / elapsed / 2**30
-    kname = f"checksum_batch_kernel<{'VALIDATE' if mode == MODE_VALIDATE else 'L4_FILL'},{_tune_tag()},nt>"
+    kname = kernel_name(mode)
     # also the L4-segment-only rate (frame bytes past csum_start)
     l4_frac = float((pkts_np["len"].astype(np.int64) - pkts_np["csum_start"].astype(np.int64)).sum()) / bytes_per_step
     result = {
@@ -292,47 +235,246 @@ def main():
             "parallelism": f"shard{world} (no collective)",
         },
     }
+    if world > 1:
+        result["config"]["dist"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                                    "gpus_visible": torch.cuda.device_count(), "device_of_rank0": local}
+    if affinity is not None:
+        result["config"]["affinity"] = affinity
     if kern_ms is not None:
         # host-side time inside the timed region beyond the GPU's event span:
         # first-launch latency + the completion wait (this rank; `value` uses the max over ranks)
         result["timing"] = {"wall_us": round(local_elapsed * 1e6, 2), "event_span_us": round(kern_ms * args.steps * 1e3, 2),
                             "wall_minus_span_us": round((local_elapsed - kern_ms * args.steps * 1e-3) * 1e6, 2),
                             "enqueue": "one wgcs_checksum_batches call for the K steps"}
-        if repeats:
+        if leg["repeats"]:
             result["timing"]["repeats"] = [{"wall_us": round(w * 1e6, 1), "event_span_us": round(m * args.steps * 1e3, 1)}
-                                           for w, m in repeats]
-        achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
-        result["roofline"] = {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic.per_launch(kname, bytes_per_step),
-            "kernel": kname,
-            "kernel_ms": round(kern_ms, 5),
-            "kernel_ms_is": ("GPU time per launch over the timed region (HIP events on the launch streams)"
-                             + (f"; {S} streams, consecutive launches overlap" if S > 1 else "")),
-            "algorithmic_bytes_per_launch": bytes_per_step,
-            "algorithmic_bytes_per_unit": flen,
-            "units_per_launch": n,
-        }
-        if iso_ms is not None:
-            result["roofline"]["kernel_ms_one_stream"] = round(iso_ms, 5)
-            result["roofline"]["frac_one_stream"] = round(bytes_per_step / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                           for w, m in leg["repeats"]]
+        result["roofline"] = roofline(kname, bytes_per_step, flen, n, kern_ms, S, iso_ms, kern_all)
     if not args.no_e2e:  # every rank moves its own shard over its own PCIe link; rank 0 reports the aggregate
         e2e = end_to_end(torch, dev, arena_np, pkts_np, mode, barrier, dist, red_dev, world)
         if rank == 0:
             result["end_to_end"] = e2e
     if rank == 0 and world == 1 and args.config == "cfg1" and not args.no_e2e:
         result["host_call"] = host_call(dev, arena_np, pkts_np, mode)
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    del leg
+    # BASELINE.json configs[4] in the same run: the 1,048,576-frame mixed batch
+    # split over the N ranks by bytes (strong scaling), its own roofline
+    if args.config == "cfg2" and not args.no_strong:
+        strong = strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_events)
+        if rank == 0:
+            result["cfg5_strong"] = strong
+    # the CPU baseline on rank 0 at every N (north_star: "reported in the same run")
+    if rank == 0 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(arena_np, pkts_np, mode, args.cpu_seconds)
+    barrier()  # the other ranks wait for rank 0's CPU leg before tearing down
     if rank == 0:
         print(json.dumps(result), flush=True)
     dev.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+REQUIRED_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                 "scaling", "vs_baseline", "dtype", "data", "config")
+
+
+def line_problems(line: dict) -> list[str]:
+    """What is missing from a cfg2 result line (the driver's default
+    invocation), per the bench contract: the required keys, `roofline`,
+    `cpu_baseline` at every N, and for N > 1 every rank's kernel time, the
+    process group's world size and the `cfg5_strong` block (BASELINE.json
+    configs[4]) with its own roofline.  Empty = complete."""
+    bad = [f"missing {k}" for k in REQUIRED_KEYS if k not in line]
+    if bad:
+        return bad
+    n = line["n_gpus"]
+    rf = line.get("roofline")
+    if not rf:
+        bad.append("missing roofline")
+    else:
+        for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+            if k not in rf:
+                bad.append(f"roofline missing {k}")
+        if n > 1 and len(rf.get("kernel_ms_per_rank", [])) != n:
+            bad.append("roofline.kernel_ms_per_rank must list every rank")
+    cb = line.get("cpu_baseline")
+    if not cb or not all(k in cb for k in ("value", "unit", "cores", "kind", "sample")):
+        bad.append("cpu_baseline missing or incomplete")
+    if n > 1:
+        d = line["config"].get("dist", {})
+        if d.get("world_size") != n:
+            bad.append("config.dist.world_size must equal n_gpus")
+    st = line.get("cfg5_strong")
+    if st is None:
+        bad.append("missing cfg5_strong")
+    else:
+        if st.get("n_gpus") != n or st.get("scaling") != "strong" or not st.get("value"):
+            bad.append("cfg5_strong: n_gpus / scaling / value")
+        if len(st.get("packets_per_rank", [])) != n or sum(st.get("packets_per_rank", [])) != CONFIGS["cfg5"][0]:
+            bad.append("cfg5_strong.packets_per_rank must cover the 1M batch")
+        srf = st.get("roofline")
+        if not srf or "frac" not in srf or (n > 1 and len(srf.get("kernel_ms_per_rank", [])) != n):
+            bad.append("cfg5_strong.roofline missing or without every rank")
+    return bad
+
+
+def kernel_name(mode) -> str:
+    from wireguard_amd.tun import MODE_VALIDATE
+
+    return f"checksum_batch_kernel<{'VALIDATE' if mode == MODE_VALIDATE else 'L4_FILL'},{_tune_tag()},nt>"
+
+
+def roofline(kname, bytes_per_step, flen, n, kern_ms, S, iso_ms, kern_all=None) -> dict:
+    """The line's `roofline` object for one rank's checksum launches (kern_ms =
+    HIP-event GPU time per launch); kern_all = every rank's kern_ms (N > 1)."""
+    from wireguard_amd import traffic
+
+    achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
+    r = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic.per_launch(kname, bytes_per_step),
+        "kernel": kname,
+        "kernel_ms": round(kern_ms, 5),
+        "kernel_ms_is": ("GPU time per launch over the timed region (HIP events on the launch streams)"
+                         + (f"; {S} streams, consecutive launches overlap" if S > 1 else "")
+                         + ("; rank 0's, every rank's in kernel_ms_per_rank" if kern_all and len(kern_all) > 1 else "")),
+        "algorithmic_bytes_per_launch": bytes_per_step,
+        "algorithmic_bytes_per_unit": flen,
+        "units_per_launch": n,
+    }
+    if kern_all and len(kern_all) > 1:
+        r["kernel_ms_per_rank"] = [round(k, 5) for k in kern_all]
+        r["kernel_ms_min"] = round(min(kern_all), 5)
+        r["kernel_ms_max"] = round(max(kern_all), 5)
+        r["frac_slowest_rank"] = round(bytes_per_step / (max(kern_all) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    if iso_ms is not None:
+        r["kernel_ms_one_stream"] = round(iso_ms, 5)
+        r["frac_one_stream"] = round(bytes_per_step / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    return r
+
+
+def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, rotate, barrier, use_events,
+                 repeat=1, verify=False, iso=True):
+    """Time `steps` checksum launches (one batch each, inputs resident in HBM)
+    after `warmup` untimed ones.  Returns {elapsed (this rank's wall s),
+    kern_ms (HIP events, GPU ms per launch), iso_ms (one-stream reference),
+    repeats, streams, R}."""
+    from wireguard_amd.tun import MODE_VALIDATE
+
+    n = len(pkts_np)
+    flen = int(pkts_np["len"][0]) if n else 0
+    bytes_per_step = int(pkts_np["len"].astype(np.int64).sum())
+    # Consecutive steps are independent batches (their own rotated arena and
+    # output), launched round-robin over S streams: step k+1's kernel streams
+    # while step k's drains and pays its end-of-kernel L2 writeback, which a
+    # single stream serialises (~1.7 us per boundary, MI355X_MICROARCH.md).
+    S = max(1, streams)
+    strm = [torch.cuda.Stream() for _ in range(S)]
+    R = rotate if bytes_per_step * rotate > (300 << 20) else max(rotate, (400 << 20) // max(bytes_per_step, 1))
+    R = max(R, 2 * S)
+    arenas = [torch.from_numpy(arena_np).to("cuda") for _ in range(R)]
+    pkts = torch.from_numpy(pkts_np.view(np.uint8)).to("cuda")
+    outs = [torch.empty(max(n, 1) * 2, dtype=torch.uint8, device="cuda") for _ in range(R)]
+    torch.cuda.synchronize()
+
+    def batches(K, k0):  # steps k0 .. k0+K-1: each its own rotated arena and output
+        return dev.batch_list([(arenas[(k0 + k) % R], pkts, n, outs[(k0 + k) % R]) for k in range(K)])
+
+    # The K steps are enqueued by ONE library call (wgcs_checksum_batches: step k
+    # on stream k % S), which also records the HIP bracket events on the launch
+    # streams: e0 on stream 0 before the first launch (the others wait on it),
+    # every other stream joined to stream 0 before e1, so (e1 - e0) / K is the
+    # GPU time per launch over the timed region.  One call instead of K Python
+    # calls: the first launch leaves the host ~10 us sooner and no per-step
+    # ctypes/torch path runs inside the region.
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(strm[0])  # torch creates the HIP events on their first record
+    e1.record(strm[0])
+
+    def timed(K, k0, ns):
+        bl = batches(K, k0)  # the step list (pointers only) is built before the clock starts
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dev.checksum_batches(mode, bl, strm[:ns], e0 if use_events else None, e1 if use_events else None)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0  # the closing barrier is not timed: max over ranks covers skew
+        barrier()
+        return el, (e0.elapsed_time(e1) / K if use_events else None)
+
+    # The one-stream reference (untimed for `value`) runs first, before the
+    # timed region's own W warmup steps: measured after a two-stream burst, the
+    # same launches read ~2-3 us slower per launch than in a one-stream
+    # process (profiles/r2_probe_iso_order.txt).  Then W warmup steps and
+    # exactly K timed steps, as the bench contract has it.
+    iso_first = os.environ.get("WGCS_ISO_FIRST", "1") == "1"
+    iso_ms = None
+    if iso and use_events and S > 1 and iso_first:
+        dev.checksum_batches(mode, batches(min(warmup, 5), 0), strm[:1])
+        _, iso_ms = timed(max(steps, 20), 0, 1)
+    # W warmup steps, enqueued exactly as the timed steps are (one call, the
+    # same streams, the same bracket events): the first cross-stream wait and
+    # join on a stream costs ~40 us once per process (profiles/r3_probe_first_region.txt)
+    if warmup > 0:
+        dev.checksum_batches(mode, batches(warmup, 0), strm, e0 if use_events else None,
+                             e1 if use_events else None)
+    torch.cuda.synchronize()
+    if verify:
+        if mode == MODE_VALIDATE:
+            assert bool(outs[0][:n].all().item()), "VALIDATE: synthetic frames must all be valid"
+        else:  # L4 fill of a valid frame reproduces the stored checksum field
+            got = outs[0].cpu().numpy().view(np.uint16)[:n]
+            a = arena_np[: n * flen].reshape(n, flen)
+            cs = pkts_np["csum_start"].astype(np.int64) + pkts_np["csum_offset"]
+            want = (a[np.arange(n), cs].astype(np.uint16) << 8) | a[np.arange(n), cs + 1]
+            assert np.array_equal(got, want), "L4_FILL mismatch vs stored checksums"
+
+    local_elapsed, kern_ms = timed(steps, warmup, S)
+    repeats = [timed(steps, warmup + r * steps, S) for r in range(1, repeat)]
+    if iso and use_events and S > 1 and not iso_first:  # the same launches one at a time on one stream
+        _, iso_ms = timed(max(steps, 20), warmup + steps, 1)
+    del arenas, outs, pkts
+    return {"elapsed": local_elapsed, "kern_ms": kern_ms, "iso_ms": iso_ms, "repeats": repeats, "streams": S, "R": R}
+
+
+def strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_events) -> dict:
+    """BASELINE.json configs[4]: the seeded 1,048,576 x 1500-B mixed
+    TCP4/UDP4/TCP6/UDP6 batch split over the `world` ranks by bytes
+    (shard.make_global_shard; no collective), K launches per rank on one
+    stream (0.27-ms launches at N=1 gain nothing from overlap).  Value =
+    the whole batch's bytes x K / the slowest rank's wall time."""
+    from wireguard_amd import shard
+
+    n_cfg, flen, kinds, cfg_idx, _ = CONFIGS["cfg5"]
+    arena_np, pkts_np, _, lo, hi = shard.make_global_shard(n_cfg, rank, world, flen, kinds)
+    bytes_rank = int(pkts_np["len"].astype(np.int64).sum())
+    leg = checksum_leg(torch, dev, arena_np, pkts_np, mode, args.steps, args.warmup, 1, 2, barrier, use_events,
+                       iso=False)
+    del arena_np
+    elapsed = shard.max_over_ranks(leg["elapsed"], dist, device=red_dev)
+    kern_all = shard.gather_floats(leg["kern_ms"] if leg["kern_ms"] is not None else -1.0, dist, device=red_dev)
+    ranges = shard.gather_floats(float(hi - lo), dist, device=red_dev)
+    out = {
+        "value": round(n_cfg * flen * args.steps / elapsed / 2**30, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "scaling": "strong",
+        "workload": f"{n_cfg} x {flen}-B {kinds} (25 % each TCP4/UDP4/TCP6/UDP6) frames split by bytes over "
+                    f"{world} GPU(s), {MODE_DESC[args.mode]} per step, BASELINE.json configs[{cfg_idx}]",
+        "packets_per_rank": [int(x) for x in ranges],
+        "streams": 1,
+        "rotated_copies": leg["R"],
+    }
+    if leg["kern_ms"] is not None:
+        out["roofline"] = roofline(kernel_name(mode), bytes_rank, flen, hi - lo, leg["kern_ms"], 1, None, kern_all)
+    return out
 
 
 def _tune_tag():

@@ -139,8 +139,13 @@ typedef struct wgcs_gso_job {
 int wgcs_abi_version(void);
 int wgcs_device_count(int *count);
 int wgcs_init(int device, wgcs_ctx **out);
+/* INVALID_ARG (the context stays usable) while a read or write stager made
+ * on it is alive: destroy the stagers first. */
 int wgcs_destroy(wgcs_ctx *ctx);
 const char *wgcs_strerror(int status);
+/* The calling thread's last error message on ctx (like errno: per thread, so
+ * concurrent callers never share one buffer); "" when this thread's last
+ * failure was on another context.  Valid until the thread's next failing call. */
 const char *wgcs_last_error(wgcs_ctx *ctx);
 int wgcs_sync(wgcs_ctx *ctx);
 /* CU count of the context's device (grid sizing, reporting) */
@@ -148,6 +153,10 @@ int wgcs_num_cu(wgcs_ctx *ctx);
 /* Pinned host memory mapped into the device's address space at the same
  * address (bytes rounded up to 16): the buffers of wgcs_wstager_push_pinned. */
 int wgcs_host_alloc(wgcs_ctx *ctx, size_t bytes, void **p);
+/* NOT_READY while a write-stager slot still reads the allocation (a recorded
+ * zero-copy push, open or in flight); safe against concurrent
+ * wgcs_wstager_push_pinned calls: either the push is refused (INVALID_ARG) or
+ * the free is (NOT_READY). */
 int wgcs_host_free(wgcs_ctx *ctx, void *p);
 
 /* ---- device-resident batch entry points (HBM in, HBM out; async on stream) ----

@@ -7,7 +7,7 @@ set -o pipefail
 CFG=${CFG:-cfg2}; ROUNDS=${ROUNDS:-3}; EXTRA=${EXTRA:-}
 for r in $(seq 1 "$ROUNDS"); do
   for lib in "$@"; do
-    line=$(WGCS_LIB="$lib" timeout -k 10 120 python bench.py --config "$CFG" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e $EXTRA 2>/dev/null | grep '^{') || exit 1
+    line=$(WGCS_LIB="$lib" WGCS_LIB_PARTIAL=1 timeout -k 10 120 python bench.py --config "$CFG" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e $EXTRA 2>/dev/null | grep '^{') || exit 1
     echo "{\"lib\": \"$(basename "$lib")\", \"round\": $r, \"line\": $line}"
   done
 done

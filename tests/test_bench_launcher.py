@@ -62,15 +62,119 @@ def test_launcher_command_runs_n_ranks(tmp_path):
     assert all(l["world"] == 2 and l["argv"] == ["--gpus", "2", "--steps", "3"] for l in lines)
 
 
+def _line(n, with_strong=True, with_cpu=True):
+    """A cfg2 line shaped as bench.main assembles it (roofline from
+    bench.roofline with every rank's kernel time)."""
+    ks = [0.0150 + 0.0001 * r for r in range(n)]
+    line = {k: 1 for k in bench.REQUIRED_KEYS}
+    line.update(n_gpus=n, value=5500.0 * n, scaling="weak",
+                config={"workload": "cfg2", "dist": {"backend": "nccl", "world_size": n}} if n > 1 else {"workload": "cfg2"},
+                roofline=bench.roofline("checksum_batch_kernel<VALIDATE,32,4,nt>", 98304000, 1500, 65536, ks[0], 2,
+                                        0.0176, ks))
+    if with_cpu:
+        line["cpu_baseline"] = {"value": 8.8, "unit": "GiB/s", "cores": 1, "kind": "port", "sample": "s"}
+    if with_strong:
+        per = [1048576 * (r + 1) // n - 1048576 * r // n for r in range(n)]
+        line["cfg5_strong"] = {"value": 5000.0 * n, "n_gpus": n, "scaling": "strong", "packets_per_rank": per,
+                               "roofline": bench.roofline("k", per[0] * 1500, 1500, per[0], 0.27 / n, 1, None,
+                                                          [0.27 / n] * n)}
+    return line
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
+def test_line_schema_complete(n):
+    """bench.line_problems accepts a complete line at every N: cpu_baseline on
+    rank 0 at every N, every rank's kernel time, the world size and the
+    configs[4] strong-scaling block."""
+    line = _line(n)
+    assert bench.line_problems(line) == []
+    if n > 1:
+        assert line["roofline"]["kernel_ms_max"] >= line["roofline"]["kernel_ms_min"]
+        assert len(line["roofline"]["kernel_ms_per_rank"]) == n
+
+
+@pytest.mark.parametrize("n", [1, 4])
+def test_line_schema_flags_gaps(n):
+    assert "missing cfg5_strong" in bench.line_problems(_line(n, with_strong=False))
+    assert "cpu_baseline missing or incomplete" in bench.line_problems(_line(n, with_cpu=False))
+    if n > 1:
+        line = _line(n)
+        line["roofline"]["kernel_ms_per_rank"] = line["roofline"]["kernel_ms_per_rank"][:1]
+        assert bench.line_problems(line) == ["roofline.kernel_ms_per_rank must list every rank"]
+        line = _line(n)
+        line["config"]["dist"]["world_size"] = 1
+        assert bench.line_problems(line) == ["config.dist.world_size must equal n_gpus"]
+
+
+def test_recorded_rehearsal_lines_complete():
+    """The N > 1 lines recorded on the GPU box (gloo ranks sharing one GPU,
+    profiles/r4_rehearse_gpus*.jsonl) are complete by the same check."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r4_rehearse_gpus*_gloo.jsonl")))
+    if not files:
+        pytest.skip("no rehearsal lines recorded yet")
+    for fn in files:
+        with open(fn) as f:
+            for l in f:
+                if l.startswith("{"):
+                    line = json.loads(l)
+                    assert line["n_gpus"] > 1
+                    assert bench.line_problems(line) == [], fn
+
+
+def test_numa_helpers(tmp_path):
+    from wireguard_amd import shard
+
+    assert shard.parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert shard.parse_cpulist("") == set()
+
+    class P:
+        pci_domain_id, pci_bus_id, pci_device_id = 0, 0x75, 0
+
+    d = tmp_path / "0000:75:00.0"
+    d.mkdir()
+    (d / "local_cpulist").write_text("0-7\n")
+    cpus, where = shard.gpu_local_cpus(P, sysfs=str(tmp_path))
+    assert cpus == set(range(8)) and where == "0000:75:00.0"
+    assert shard.gpu_local_cpus(object())[0] is None
+
+
+def test_gather_floats_gloo():
+    """Every rank's kernel time reaches rank 0 (the N > 1 line's
+    kernel_ms_per_rank), over gloo world 2 on the CPU."""
+    import torch.multiprocessing as mp
+
+    port = bench._free_port()
+    mp.spawn(_gather_worker, args=(2, port), nprocs=2, join=True)
+
+
+def _gather_worker(rank, world, port):
+    import torch.distributed as dist
+
+    from wireguard_amd import shard
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        got = shard.gather_floats(0.5 + rank, dist)
+        assert got == [0.5, 1.5], got
+        assert shard.max_over_ranks(0.5 + rank, dist) == 1.5
+    finally:
+        dist.destroy_process_group()
+
+
 @pytest.mark.gpu
-def test_bench_gpus2_runs_two_ranks():
-    """`python bench.py --gpus 2` with no launcher: two gloo ranks sharing
-    cuda:0 (WGCS_DIST_BACKEND=gloo), one result line with n_gpus == 2."""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5",
-                        "--warmup", "2", "--cpu-seconds", "0", "--no-e2e"], cwd=ROOT,
+@pytest.mark.parametrize("n", [2])
+def test_bench_gpus_n_runs_n_ranks(n):
+    """`python bench.py --gpus N` with no launcher: N gloo ranks sharing
+    cuda:0 (WGCS_DIST_BACKEND=gloo), one complete result line (cfg5_strong,
+    cpu_baseline, every rank's kernel time)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "5",
+                        "--warmup", "2", "--cpu-seconds", "0.5", "--no-e2e"], cwd=ROOT,
                        env=_env(WGCS_DIST_BACKEND="gloo"), capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
-    assert lines[0]["n_gpus"] == 2 and lines[0]["value"] > 0
-    assert lines[0]["config"]["parallelism"] == "shard2 (no collective)"
+    assert lines[0]["n_gpus"] == n and lines[0]["value"] > 0
+    assert lines[0]["config"]["parallelism"] == f"shard{n} (no collective)"
+    assert bench.line_problems(lines[0]) == []

@@ -90,7 +90,7 @@ def test_gro_batch_matches_handle_gro(dev, seed):
     assert _check(dev, calls) == len(calls)
 
 
-def test_gro_batch_edge_calls(dev):
+def edge_calls():
     f4 = flow(8, seg=1448, seed=7)
     f6 = flow(8, seg=1000, v6=True, seed=8)
     u4 = flow(8, seg=1200, udp=True, seed=9)
@@ -106,10 +106,15 @@ def test_gro_batch_edge_calls(dev):
         (f4 + u4, 65535, True, {5: 3}),                 # invalid offset part-way (len < offset)
         ([bytes(40)] * 4 + f4, 65535, True, None),      # non-candidates first
     ]
+    return calls
+
+
+def test_gro_batch_edge_calls(dev):
+    calls = edge_calls()
     assert _check(dev, calls) == len(calls)
 
 
-def test_gro_batch_bad_checksums_and_flags(dev):
+def bad_checksum_calls():
     rng = np.random.default_rng(5)
     calls = []
     for k in range(12):
@@ -123,6 +128,11 @@ def test_gro_batch_bad_checksums_and_flags(dev):
             pk[i] = bytes(b)
         order = np.argsort(rng.random(len(pk)) + np.arange(len(pk)) * 0.05)
         calls.append(([pk[i] for i in order], 65535, True, None))
+    return calls
+
+
+def test_gro_batch_bad_checksums_and_flags(dev):
+    calls = bad_checksum_calls()
     assert _check(dev, calls) == len(calls)
 
 
@@ -134,9 +144,9 @@ def test_gro_batch_rejects_oversized_call(dev):
     assert np.array_equal(arena, arena0)
 
 
-def test_gro_batch_host_test_scenarios(dev):
+def host_scenario_calls():
     """Every scenario of tests/test_gpu_gro.py (the host-path GRO tests) as
-    one call each, all in one launch."""
+    one call each."""
     rng = np.random.default_rng(11)
     s_pre = flow(6, seed=3)
     s_bad = flow(8, seed=5)
@@ -180,6 +190,12 @@ def test_gro_batch_host_test_scenarios(dev):
         ([big[i] for i in perm], 65535, True, None),
         (big, 65535, True, None),
     ] + [(inv, 65535, True, {bad_at: OFFSET}) for bad_at in (1, 5, 9, 13)]
+    return calls
+
+
+def test_gro_batch_host_test_scenarios(dev):
+    """Every scenario of tests/test_gpu_gro.py as one call each, all in one launch."""
+    calls = host_scenario_calls()
     assert _check(dev, calls) == len(calls)
 
 
@@ -216,12 +232,11 @@ def _opt_flow(rng, nseg, mss, v6, same_opts, seed):
     return out
 
 
-def test_gro_batch_tcp_options_fuzz(dev):
+def tcp_options_calls():
     """Random Write calls mixing TCP flows with timestamp options (equal
     options coalesce, changing ones do not: gro.go:442-448), flows without
     options, UDP, reordering (prepends), tight capacities and corrupted
-    checksums -- the register fast path falls back to the LDS path for every
-    one of these."""
+    checksums."""
     rng = np.random.default_rng(2024)
     calls = []
     for k in range(40):
@@ -245,6 +260,71 @@ def test_gro_batch_tcp_options_fuzz(dev):
             b = bytearray(pk[i]); b[-1] ^= 0x24; pk[i] = bytes(b)
         cap = 65535 if k % 4 else (lambda n, e=int(rng.integers(0, 4000)): OFFSET + n + e)
         calls.append((pk, cap, bool(k % 5), None))
+    return calls
+
+
+def _udp_pkt(src, dst, sport, dport, payload, v6):
+    """One UDP datagram with valid IPv4 / UDP checksums (oracle checksum
+    functions: test infrastructure)."""
+    import struct
+
+    udp = bytearray(struct.pack("!HHHH", sport, dport, 8 + len(payload), 0) + payload)
+    if v6:
+        ip = bytearray(struct.pack("!IHBB", 0x60000000, len(udp), 17, 64) + src + dst)
+    else:
+        ip = bytearray(struct.pack("!BBHHHBBH4s4s", 0x45, 0, 20 + len(udp), 0x1234, 0x4000, 64, 17, 0, src, dst))
+        ip[10:12] = ((~oracle.checksum(bytes(ip), 0)) & 0xFFFF).to_bytes(2, "big")
+    c = (~oracle.checksum(bytes(udp), oracle.pseudo_header_nofold(src, dst, 17, len(udp)))) & 0xFFFF
+    udp[6:8] = c.to_bytes(2, "big")
+    return bytes(ip + udp)
+
+
+def _seq_flow(rng, nseg, mss, v6, udp=False, psh_at=(), seq0=None):
+    src = bytes(rng.integers(0, 256, 16 if v6 else 4, dtype=np.uint8))
+    dst = bytes(rng.integers(0, 256, 16 if v6 else 4, dtype=np.uint8))
+    seq0 = int(rng.integers(0, 2**32)) if seq0 is None else seq0
+    out = []
+    for k in range(nseg):
+        pay = bytes(rng.integers(0, 256, mss, dtype=np.uint8))
+        if udp:
+            out.append(_udp_pkt(src, dst, 4000, 51820, pay, v6))
+        else:
+            out.append(_tcp_pkt(src, dst, 4000, 51820, seq0 + k * mss, 0x18 if k in psh_at else 0x10, b"", pay, v6))
+    return out
+
+
+def quirk_calls():
+    """Write calls that reach the reference's integer-width quirks and PSH
+    rules: capacities above 64 KiB, so an item grows past the uint16
+    lhsLen = gsoSize * (numMerged + 1) (gro.go:468, it wraps and the next
+    segment no longer looks adjacent) and past uint16 total / payload / UDP
+    lengths (apply*, gro.go:1124-1138, :1206-1232); a PSH segment in the middle
+    of a flow (nothing appends after it, gro.go:474-478; it still appends
+    itself, :724-729); the sequence number wrapping 2^32."""
+    rng = np.random.default_rng(77)
+    big = 200000
+    return [
+        (_seq_flow(rng, 8, 1000, False, psh_at=(3,)), 65535, True, None),
+        (_seq_flow(rng, 8, 1000, True, psh_at=(0, 5)), 65535, True, None),
+        (_seq_flow(rng, 100, 1448, False), big, True, None),
+        (_seq_flow(rng, 128, 536, True), big, True, None),
+        (_seq_flow(rng, 100, 1400, False, udp=True), big, True, None),
+        (_seq_flow(rng, 60, 1200, True, udp=True), big, True, None),
+        (list(reversed(_seq_flow(rng, 60, 1448, False))), big, True, None),
+        (_seq_flow(rng, 20, 1448, False, seq0=2**32 - 5 * 1448 - 7), 65535, True, None),
+        (list(reversed(_seq_flow(rng, 20, 1000, True, seq0=2**32 - 700))), 65535, True, None),
+    ]
+
+
+def test_gro_batch_quirk_calls(dev):
+    calls = quirk_calls()
+    assert _check(dev, calls) == len(calls)
+
+
+def test_gro_batch_tcp_options_fuzz(dev):
+    """The options fuzz calls in one launch: the register fast path falls back
+    to the LDS path for every one of these."""
+    calls = tcp_options_calls()
     assert _check(dev, calls) == len(calls)
 
 

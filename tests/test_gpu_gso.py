@@ -6,6 +6,7 @@ import struct
 import numpy as np
 import pytest
 
+import gso_cases
 import oracle
 from wireguard_amd import synth
 from wireguard_amd._lib import (ERR_BAD_IP_VERSION, ERR_CSUM_OFFSET, ERR_HDR_LEN, ERR_IP_GSO_MISMATCH,
@@ -188,59 +189,17 @@ def test_validation_errors(dev):
             assert_same(o, p)
 
 
-def _fuzz_header(rng, base: bytearray, raw: bool):
-    """Mutate the virtio header / IP version / TCP data offset of a valid
-    super-packet: any header geometry handleVirtioRead or gsoSplit accepts,
-    including IP headers shorter than 20 / 40 bytes, headers over 240 bytes,
-    checksum fields outside the header, wrapped uint16 positions."""
-    b = bytearray(base)
-    plen = len(b) - 10
-    f = lambda a, v: b.__setitem__(slice(a, a + 2), int(v % 65536).to_bytes(2, "little"))  # noqa: E731
-    if rng.random() < 0.2:
-        b[0] = int(rng.integers(0, 256))
-    if rng.random() < 0.3:
-        b[1] = int(rng.choice([0, 1, 4, 5, int(rng.integers(0, 256))]))
-    cs = int(rng.choice([int.from_bytes(b[6:8], "little"), int(rng.integers(0, 64)), int(rng.integers(0, 400)),
-                         int(rng.integers(65500, 65536))], p=[0.25, 0.35, 0.35, 0.05]))
-    f(6, cs)
-    if rng.random() < 0.8 and plen >= 2:
-        at = int(rng.integers(0, min(plen - 1, 600))) if rng.random() < 0.7 else int(rng.integers(0, plen - 1))
-        f(8, at - cs)
-    else:
-        f(8, int(rng.integers(0, 65536)))
-    if rng.random() < 0.5:
-        f(2, int(rng.choice([cs + 8, cs + 20, int(rng.integers(0, 600)), int(rng.integers(0, 65536))])))
-    if rng.random() < 0.4:
-        f(4, int(rng.choice([0, 1, 7, int(rng.integers(1, 3000)), 65535])))
-    if rng.random() < 0.3:
-        b[10] = (int(rng.choice([4, 6, int(rng.integers(0, 16))])) << 4) | (b[10] & 0xF)
-    if 10 + cs + 12 < len(b) and rng.random() < 0.5:
-        b[10 + cs + 12] = int(rng.choice([0x50, 0x80, 0xF0, int(rng.integers(0, 256))]))
-    if rng.random() < 0.25:
-        b = b[: int(rng.integers(10, len(b) + 1))]
-    return bytes(b)
-
-
 @pytest.mark.parametrize("raw", [False, True])
 def test_fuzz_headers(dev, raw):
     """>= 1000 mutated headers per entry point.  The only cases not compared
     byte for byte are those where the ORACLE reports a reference panic
     (OUT_OF_RANGE); the product must report the same there."""
-    rng = np.random.default_rng(17 + raw)
-    bases = [bytearray(synth.make_super_packet(t, g, seed=t, v6=v6, udp=u))
-             for t, g, v6, u in [(8000, 1000, False, False), (3000, 500, True, False), (6000, 1448, False, True),
-                                 (2500, 700, True, True), (1200, 100, False, False), (20000, 1460, False, False)]]
     compared = panics = 0
-    trials = 1500 if raw else 1100
-    for trial in range(trials):
-        vp = _fuzz_header(rng, bases[trial % len(bases)], raw)
-        nbufs = int(rng.choice([4, 16, 64]))
-        bufsize = int(rng.choice([2000, 9000, 65535]))
-        fill = int(rng.choice([SENT, 0x00, 0xFF]))
-        offset = int(rng.choice([16, 10, 3, 0]))
+    trials = 0
+    for trial, (vp, nbufs, bufsize, fill, offset, h, is_v6) in enumerate(gso_cases.fuzz_cases(raw)):
+        trials += 1
         if raw:
-            h = tuple([vp[0], vp[1]] + [int.from_bytes(vp[k:k + 2], "little") for k in (2, 4, 6, 8)])
-            o, p = run_both_raw(dev, vp[10:], h, bool(rng.integers(0, 2)), nbufs, bufsize, offset, fill)
+            o, p = run_both_raw(dev, vp[10:], h, is_v6, nbufs, bufsize, offset, fill)
         else:
             o, p = run_both(dev, vp, nbufs, bufsize, offset, fill)
         if o[0] == ERR_OUT_OF_RANGE:
@@ -249,7 +208,7 @@ def test_fuzz_headers(dev, raw):
             continue
         assert_same(o, p, check_bufs="packets", offset=offset, fill=fill)
         compared += 1
-    assert compared >= 550 and compared + panics == trials
+    assert compared >= 550 and compared + panics == trials == (1500 if raw else 1100)
 
 
 def test_general_path_geometries(dev):
@@ -390,3 +349,55 @@ def test_batch_rejects_huge_max_segs(dev):
     with pytest.raises(WgcsError) as ei:
         dev.gso_split_batch(small, small, 1, small, 16, 0, 1 << 31, i32, i32, i32)
     assert ei.value.code == -1  # WGCS_ERR_INVALID_ARG
+
+
+def test_batch_invalid_jobs_large_max_segs_return_promptly(dev):
+    """A job that is not a split (GSO_NONE, bad gso type, IP-version mismatch,
+    jlen < 14) under a large max_segs: the decoded path's verdict ends the
+    block's group loop after the first group instead of running one decode +
+    barrier round per 16 output slots.  Results vs the oracle,
+    and the launch must take far less than the ~0.5 s those rounds would."""
+    import time
+
+    import torch
+
+    pkt = bytearray(synth.make_super_packet(1500, 1460, seed=43))
+    none_job = bytes([1, 0]) + bytes(pkt[2:10]) + bytes(pkt[10:])  # GSO_NONE + NEEDS_CSUM
+    bad_type = bytes([1, 3]) + bytes(pkt[2:])
+    v6_mismatch = bytes([1, 4]) + bytes(pkt[2:])  # TCPV6 on an IPv4 packet
+    short = bytes(pkt[:12])
+    vps = [none_job, bad_type, v6_mismatch, short]
+    offs = np.cumsum([0] + [len(v) + 5 for v in vps])[:-1]
+    arena = np.zeros(int(offs[-1]) + len(vps[-1]) + 64, np.uint8)
+    for o_, v in zip(offs, vps):
+        arena[o_: o_ + len(v)] = np.frombuffer(v, np.uint8)
+    jobs = np.zeros(len(vps), GSO_JOB_DTYPE)
+    jobs["off"] = offs
+    jobs["len"] = [len(v) for v in vps]
+    offset, stride = 16, 1600
+    d_arena = torch.from_numpy(arena).cuda()
+    d_jobs = torch.from_numpy(jobs.view(np.uint8)).cuda()
+    d_count = torch.zeros(len(vps), dtype=torch.int32, device="cuda")
+    d_status = torch.zeros(len(vps), dtype=torch.int32, device="cuda")
+    for max_segs in (16, 1 << 24):
+        # only job 0 (GSO_NONE) writes: bufs[0] at slot 0, sizes[0]
+        d_out = torch.full((stride,), SENT, dtype=torch.uint8, device="cuda")
+        d_sizes = torch.full((len(vps) * max_segs,), -7, dtype=torch.int32, device="cuda")
+        dev.sync()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dev.gso_split_batch(d_arena, d_jobs, len(vps), d_out, stride, offset, max_segs, d_sizes, d_count, d_status)
+        dev.sync()
+        dt = time.perf_counter() - t0
+        assert dt < 0.1, (max_segs, dt)
+        count, status = d_count.cpu().numpy(), d_status.cpu().numpy()
+        for j, v in enumerate(vps):
+            rb = np.frombuffer(bytearray(v), np.uint8).copy()
+            bo = _bufs(min(max_segs, 4), stride)
+            rc, n_o, sz_o = oracle.handle_virtio_read(rb, bo, offset)
+            assert status[j] == rc and count[j] == n_o, (j, max_segs)
+            if j == 0:
+                assert rc == 0 and n_o == 1
+                assert int(d_sizes[0].item()) == sz_o[0]
+                assert np.array_equal(d_out.cpu().numpy(), bo[0])
+        assert int((d_sizes[1:] != -7).sum().item()) == 0  # nothing else written

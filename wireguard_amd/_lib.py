@@ -132,9 +132,20 @@ def load() -> C.CDLL:
         "wgcs_wstager_result": ([vp, u64, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(vp),
                                  C.POINTER(sz)], i32),
     }
+    missing = [name for name in sig if not hasattr(L, name)]
+    if missing:
+        # only an explicit A/B build of an older revision may lack entry points
+        # (scripts/probe_lib_bench.sh sets WGCS_LIB_PARTIAL=1); anything else
+        # fails here, at load, not later at the first call
+        if os.environ.get("WGCS_LIB_PARTIAL") != "1":
+            raise RuntimeError(f"{LIB_PATH}: missing wgcsum entry points {missing} (a stale or mismatched library; "
+                               "rebuild with `python -m wireguard_amd.build`)")
+        import warnings
+
+        warnings.warn(f"{LIB_PATH}: partial A/B library without {missing}", RuntimeWarning, stacklevel=2)
     for name, (args, res) in sig.items():
-        if os.environ.get("WGCS_LIB") and not hasattr(L, name):
-            continue  # an A/B build of an older revision (scripts/probe_lib_bench.sh)
+        if name in missing:
+            continue
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res

@@ -21,14 +21,22 @@ using namespace wgcs;
 
 namespace wgcs {
 
+// The last error message is per calling thread (like errno): concurrent
+// callers of one context (Tun.Write runs on many goroutines, tun.go:654-700)
+// never write one shared string, and the pointer wgcs_last_error returns stays
+// valid until the same thread's next failing call.
+namespace {
+thread_local const wgcs_ctx* tls_err_ctx = nullptr;
+thread_local char tls_err[512];
+}  // namespace
+
 int set_err(wgcs_ctx* ctx, int code, const char* fmt, ...) {
   if (ctx) {
-    char buf[512];
     va_list ap;
     va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
+    vsnprintf(tls_err, sizeof tls_err, fmt, ap);
     va_end(ap);
-    ctx->last_error = buf;
+    tls_err_ctx = ctx;
   }
   return code;
 }
@@ -70,12 +78,16 @@ int ensure_pinned(wgcs_ctx* ctx, HostBuf& b, size_t bytes) {
   return WGCS_OK;
 }
 
-bool host_mapped(wgcs_ctx* ctx, const void* p, size_t n) {
+bool host_mapped_locked(wgcs_ctx* ctx, const void* p, size_t n) {
   const uintptr_t a = (uintptr_t)p, b = a + n;
-  std::lock_guard<std::mutex> g(ctx->host_mu);
   for (const auto& r : ctx->host_allocs)
     if (a >= r.first && b <= r.second && b >= a) return true;
   return false;
+}
+
+bool host_mapped(wgcs_ctx* ctx, const void* p, size_t n) {
+  std::lock_guard<std::mutex> g(ctx->host_mu);
+  return host_mapped_locked(ctx, p, n);
 }
 
 }  // namespace wgcs
@@ -187,9 +199,12 @@ int wgcs_destroy(wgcs_ctx* ctx) {
   if (!ctx) return WGCS_ERR_INVALID_ARG;
   {
     std::lock_guard<std::mutex> g(ctx->host_mu);
-    if (!ctx->wstagers.empty())  // their slots use the context and may read its host allocations
-      return set_err(ctx, WGCS_ERR_INVALID_ARG, "wgcs_destroy: %zu write stager(s) still alive: destroy them first",
-                     ctx->wstagers.size());
+    // stagers keep the context (its device, staging and error state) and
+    // write stagers' slots may read its host allocations
+    if (!ctx->wstagers.empty() || !ctx->stagers.empty())
+      return set_err(ctx, WGCS_ERR_INVALID_ARG,
+                     "wgcs_destroy: %zu read stager(s) and %zu write stager(s) still alive: destroy them first",
+                     ctx->stagers.size(), ctx->wstagers.size());
   }
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
@@ -232,7 +247,7 @@ const char* wgcs_strerror(int status) {
   }
 }
 
-const char* wgcs_last_error(wgcs_ctx* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+const char* wgcs_last_error(wgcs_ctx* ctx) { return ctx && tls_err_ctx == ctx ? tls_err : ""; }
 
 int wgcs_num_cu(wgcs_ctx* ctx) { return ctx ? ctx->num_cu : WGCS_ERR_INVALID_ARG; }
 

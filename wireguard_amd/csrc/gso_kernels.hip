@@ -772,8 +772,11 @@ __device__ __forceinline__ void finish_row(bool fast, const uint4 Q, int type, i
 // runs the full validation (decode_publish) and publishes its verdict through
 // LDS, the rows follow it.  Out of line, so that its registers do not count
 // against the clean path's occupancy (it spills, if at all, only here).
+// Returns the job's live segment count from the published verdict (0 for an
+// error, GSO_NONE or no segment): block-uniform, so the caller's group loop
+// stops after the last group that holds a segment.
 template <int U, bool NT>
-__device__ __noinline__ void decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, uint32_t jflags_a, uint32_t room,
+__device__ __noinline__ int decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, uint32_t jflags_a, uint32_t room,
                                           uint32_t max_segs, int i, bool first_block, int32_t* count_j,
                                           int32_t* status_j, uint8_t* out0, uint8_t* dst, int32_t* sizes_j) {
   __shared__ JobInfo ji;
@@ -798,7 +801,7 @@ __device__ __noinline__ void decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, 
   const int nseg = ufl(ji.nseg);
   const uint32_t shape = (uint32_t)ufl((int)ji.shape);
   const int type = (int)(shape & 0xFFu);
-  if ((st != 0 && st != WGCS_ERR_TOO_MANY_SEGMENTS) || nseg == 0) return;
+  if ((st != 0 && st != WGCS_ERR_TOO_MANY_SEGMENTS) || nseg == 0) return 0;
   const int plen = ufl(ji.plen);
   if (type == GSO_NONE) {  // one packet into bufs[0], by wave 0 of the job's first block
     if (first_block && wv == 0) {
@@ -810,9 +813,9 @@ __device__ __noinline__ void decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, 
       none_segment(rb, jn, out0, lane);
       if (lane == 0) *sizes_j = plen;
     }
-    return;
+    return 0;
   }
-  if (i >= nseg) return;  // whole rows retire; DPP below stays inside live rows
+  if (i >= nseg) return nseg;  // whole rows retire; DPP below stays inside live rows
   const int ipv = (int)((shape >> 8) & 0xFFu);
   const bool fast = (shape >> 24) != 0;
   const int hdr_len = ufl(ji.hdr_len);
@@ -821,7 +824,7 @@ __device__ __noinline__ void decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, 
   const int co = ufl(ji.co);
   if ((shape >> 16) & 0xFFu) {  // block-uniform
     gso_general_row(rb, plen, type, ipv, hdr_len, gso, cs, co, i, dst, r, sizes_j + i);
-    return;
+    return nseg;
   }
   uint32_t acc = 0;
   stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen));
@@ -841,6 +844,7 @@ __device__ __noinline__ void decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, 
   const uint32_t seq0 = (uint32_t)ufl((int)ji.seq0);
   finish_row(fast, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base, tflags,
              id0, seq0, sizes_j + i);
+  return nseg;
 }
 
 // Build-time tunables (defaults measured on cfg4):
@@ -1050,9 +1054,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
     for (int grp = (int)blockIdx.y; group_live(grp); grp += (int)gridDim.y) {  // block-uniform
       const int i = grp * ROWS + wv * 4 + (lane >> 4);
       uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
-      decoded_rows<U, NT>(vb, jlen, job.flags, room, max_segs, i, grp == 0, &count[jb], &status[jb],
-                          out + obase + offset, dst, &sizes[slot0]);
+      const int live = decoded_rows<U, NT>(vb, jlen, job.flags, room, max_segs, i, grp == 0, &count[jb], &status[jb],
+                                           out + obase + offset, dst, &sizes[slot0]);
       lds_barrier();  // every wave is done with this group's verdict before the next one is published
+      // the verdict bounds the job's segments (0 for an error / GSO_NONE): no
+      // decode + barrier round for groups past it, whatever max_segs is
+      if ((int64_t)(grp + (int)gridDim.y) * ROWS >= (int64_t)ufl(live)) break;
     }
   }
 }

@@ -202,12 +202,21 @@ int wgcs_stager_create(wgcs_ctx* ctx, uint32_t depth, uint32_t max_reads, size_t
     wgcs_stager_destroy(st);
     return rc;
   }
+  {
+    std::lock_guard<std::mutex> g(ctx->host_mu);
+    ctx->stagers.push_back(st);
+  }
   *out = st;
   return WGCS_OK;
 }
 
 int wgcs_stager_destroy(wgcs_stager* st) {
   if (!st) return WGCS_ERR_INVALID_ARG;
+  {
+    std::lock_guard<std::mutex> g(st->ctx->host_mu);
+    auto& v = st->ctx->stagers;
+    v.erase(std::remove(v.begin(), v.end(), st), v.end());
+  }
   hipSetDevice(st->ctx->device);
   for (auto& s : st->slots) {
     if (s.state == 2) hipEventSynchronize(s.done);

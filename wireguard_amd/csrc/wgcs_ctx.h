@@ -26,8 +26,10 @@ int set_err(wgcs_ctx* ctx, int code, const char* fmt, ...);
 int hip_fail(wgcs_ctx* ctx, hipError_t e, const char* what);
 int ensure_dev(wgcs_ctx* ctx, DevBuf& b, size_t bytes);
 int ensure_pinned(wgcs_ctx* ctx, HostBuf& b, size_t bytes);
-// [p, p + n) lies inside one wgcs_host_alloc allocation of ctx
+// [p, p + n) lies inside one wgcs_host_alloc allocation of ctx (the _locked
+// form: the caller holds ctx->host_mu)
 bool host_mapped(wgcs_ctx* ctx, const void* p, size_t n);
+bool host_mapped_locked(wgcs_ctx* ctx, const void* p, size_t n);
 // A live write-stager slot (open, or submitted and not yet finished) still
 // reads [a, b) through a zero-copy push (wstager.cpp); caller holds host_mu.
 bool wstager_references(wgcs_wstager* ws, uintptr_t a, uintptr_t b);
@@ -39,7 +41,6 @@ struct wgcs_ctx {
   int num_cu = 256;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  std::string last_error;
   wgcs::LaunchTuning tune;
   // device staging (grown on demand, never shrunk)
   wgcs::DevBuf d_arena, d_pkts, d_init, d_out, d_out2, d_aux;
@@ -48,8 +49,11 @@ struct wgcs_ctx {
   // stream-join events of wgcs_checksum_batches (timing disabled; [1, 16) made by wgcs_init)
   hipEvent_t join_ev[WGCS_MAX_BATCH_STREAMS] = {};
   // wgcs_host_alloc allocations (device-readable pinned memory): [start, end),
-  // and the live write stagers, whose zero-copy pushes point into them
+  // the live write stagers, whose zero-copy pushes point into them, and the
+  // live read stagers (wgcs_destroy refuses while any stager is alive).  Lock
+  // order: host_mu before a write stager's mu.
   std::mutex host_mu;
   std::vector<std::pair<uintptr_t, uintptr_t>> host_allocs;
   std::vector<wgcs_wstager*> wstagers;
+  std::vector<wgcs_stager*> stagers;
 };

@@ -293,8 +293,6 @@ int push_call(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, 
     for (int i = 0; i < n; ++i) {
       if (caps[i] < lens[i]) return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: cap(bufs[%d]) < len", i);
       total += lens[i] - offset;
-      if (pinned && !host_mapped(ws->ctx, bufs[i] + offset - kVnet, lens[i] - offset + kVnet))
-        return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: bufs[%d] is not in wgcs_host_alloc memory", i);
       if (!pinned) need += kHead + al16(lens[i] - offset);
       need_out += out_need(lens[i] - offset);
     }
@@ -306,6 +304,19 @@ int push_call(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, 
   uint8_t* stage;
   uint64_t at;
   WSlot* sp;
+  // A zero-copy push holds host_mu from its check that every buffer lies in
+  // wgcs_host_alloc memory until its moves are recorded (host_mu, then
+  // ws->mu, the order wgcs_host_free takes them): a concurrent
+  // wgcs_host_free either runs first (this push is refused) or finds the
+  // recorded moves (it returns NOT_READY); the memory is never freed under a
+  // slot that will read it.
+  std::unique_lock<std::mutex> hg(ws->ctx->host_mu, std::defer_lock);
+  if (pinned && !c.status) {
+    hg.lock();
+    for (int i = 0; i < n; ++i)
+      if (!host_mapped_locked(ws->ctx, bufs[i] + offset - kVnet, lens[i] - offset + kVnet))
+        return set_err(ws->ctx, WGCS_ERR_INVALID_ARG, "wstager: bufs[%d] is not in wgcs_host_alloc memory", i);
+  }
   {
     std::lock_guard<std::mutex> g(ws->mu);
     if (ws->broken) return set_err(ws->ctx, WGCS_ERR_HIP, "wstager unusable after a HIP error");

@@ -102,10 +102,14 @@ class Device:
         self._stagers = weakref.WeakSet()  # closed before the context (wgcs_destroy refuses live write stagers)
 
     def close(self) -> None:
+        """wgcs_destroy; raises (and keeps the context) when the library
+        refuses, e.g. while a stager made through raw lib calls is alive."""
         if self.h:
             for st in list(self._stagers):
                 st.close()
-            self.lib.wgcs_destroy(self.h)
+            rc = self.lib.wgcs_destroy(self.h)
+            if rc != 0:
+                raise WgcsError(rc, self.lib.wgcs_last_error(self.h).decode() or self.lib.wgcs_strerror(rc).decode())
             self.h = None
 
     def __del__(self):
