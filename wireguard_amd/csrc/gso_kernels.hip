@@ -538,9 +538,12 @@ __device__ __forceinline__ bool wave_none(bool pred) { return __builtin_amdgcn_b
 // registers (v_dot2) and stores the payload bytes of every chunk (those of a
 // chunk shared with the header as byte-exact pieces; the header phase stores
 // the chunk's header bytes).
-template <int U, bool NT>
+// A segment may be split over P rows (part = 0 .. P-1): part p takes the
+// batches of 16 * U chunks starting at p, p + P, ... (P = 1: the whole segment).
+template <int U, bool NT, int P = 1>
 __device__ __forceinline__ void stream_row(const uint8_t* rb, int i, int gso, int hdr_len, int plen, int dalign,
-                                           uint8_t* dbase, int r, uint32_t& acc, __amdgpu_buffer_rsrc_t rs) {
+                                           uint8_t* dbase, int r, uint32_t& acc, __amdgpu_buffer_rsrc_t rs,
+                                           int part = 0) {
   const int seg_start = hdr_len + i * gso;
   const int seg_end = min(plen, seg_start + gso);
   const int pkt_len = hdr_len + (seg_end - seg_start);
@@ -549,7 +552,7 @@ __device__ __forceinline__ void stream_row(const uint8_t* rb, int i, int gso, in
   const int sb = (int)((uintptr_t)w0 & 3u);
   const int aoff = (int)(w0 - sb - (rb - 10));         // its dword-aligned window, job-relative
   acc = 0;
-  for (int k0 = 0; k0 < nk; k0 += 16 * U) {
+  for (int k0 = 16 * U * part; k0 < nk; k0 += 16 * U * P) {
     uint4 A[U];
     uint32_t E;
     load_windows<U, NT>(rs, aoff, k0, r, 10 + seg_start, 10 + seg_end, A, E);
@@ -859,8 +862,17 @@ __device__ __noinline__ int decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, u
 #define WGCS_GSO_WAVES 5
 #endif
 #ifndef WGCS_GSO_GROUPS
-#define WGCS_GSO_GROUPS 3  // blocks per job (grid y); each takes every WGCS_GSO_GROUPS-th segment group
+#define WGCS_GSO_GROUPS 3  // blocks per job (grid y) at one row per segment; each takes every WGCS_GSO_GROUPS-th group
 #endif
+// Rows per segment on the clean path (1, 2 or 4): P rows share one segment's
+// payload stream (part p: chunk batches p, p + P, ...), so a block's 16 rows
+// hold 16 / P segments and a job needs P times the waves -- more, shorter
+// waves per launch.  The part sums meet in part 0's row (lane-wise, across
+// rows), which writes the header chunk, the checksums and the size.
+#ifndef WGCS_GSO_PARTS
+#define WGCS_GSO_PARTS 1
+#endif
+static_assert(WGCS_GSO_PARTS == 1 || WGCS_GSO_PARTS == 2 || WGCS_GSO_PARTS == 4, "WGCS_GSO_PARTS: 1, 2 or 4");
 template <int U, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WAVES, 8))) void gso_rows_kernel(const uint8_t* __restrict__ arena,
                                                        const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
@@ -868,7 +880,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
                                                        const GsoOutPos* __restrict__ outpos, uint32_t offset,
                                                        uint32_t room, int32_t* __restrict__ sizes,
                                                        int32_t* __restrict__ count, int32_t* __restrict__ status) {
-  constexpr int ROWS = 16;
+  constexpr int ROWS = 16;                    // rows per block; segments per group on the decoded path
+  constexpr int P = WGCS_GSO_PARTS;
+  constexpr int SEGS = ROWS / P;              // segments per group on the clean path
 #ifdef WGCS_GSO_STAMPS  // timing-only build (scripts/probe_gso_stamps.py): s_memrealtime per wave phase
   uint64_t stp[5] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0};
 #endif
@@ -950,13 +964,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   // Groups that may hold a segment: gbound = max(1, min(ngroups, ceil(nbound /
   // 16))) with nbound = ceil((plen - hmin) / gsoSize); group y < gbound iff y
   // == 0 or (y < ngroups and 16 y gsoSize < plen - hmin).
-  const int ngroups = (int)((max_segs + ROWS - 1) / ROWS);
+  const int ngroups = (int)((max_segs + SEGS - 1) / SEGS);
   const int hmin = raw ? (int)hl : (tcp_s ? cs_s + 20 : cs_s + 8);
   const bool split_type = jlen >= 14 && ok_s && cs_s + 60 <= 0xFFFF;
   const bool gso_none = jlen >= 14 && !raw && t1 == GSO_NONE;
   auto group_live = [&](int y) {
     if (y == 0) return true;
     if (gso_none || y >= ngroups) return false;
+    return !split_type || (plen_s > hmin && hmin + (int64_t)y * SEGS * gso_s < plen_s);
+  };
+  // the decoded path keeps one row per segment: groups of ROWS segments
+  // (a block live for them is live for the clean path's groups of SEGS)
+  const int ngroups16 = (int)((max_segs + ROWS - 1) / ROWS);
+  auto group_live16 = [&](int y) {
+    if (y == 0) return true;
+    if (gso_none || y >= ngroups16) return false;
     return !split_type || (plen_s > hmin && hmin + (int64_t)y * ROWS * gso_s < plen_s);
   };
   if (!group_live((int)blockIdx.y)) return;
@@ -1023,20 +1045,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
     if (ufl((int)(ip_base + l4_base + tflags + id0 + seq0)) == 0x7FFFFFFF) sizes[slot0] = 0;
     return;
 #endif
-    for (int grp = (int)blockIdx.y; has_seg(grp * ROWS); grp += (int)gridDim.y) {  // block-uniform
-      const int i = grp * ROWS + wv * 4 + (lane >> 4);  // this row's segment
-      if (has_seg(i)) {  // row-uniform
+    for (int grp = (int)blockIdx.y; has_seg(grp * SEGS); grp += (int)gridDim.y) {  // block-uniform
+      const int row = wv * 4 + (lane >> 4);
+      const int i = grp * SEGS + row / P;  // this row's segment
+      const int part = row % P;            // and its part of it
+      if (has_seg(i)) {  // row-uniform (the P rows of a segment agree)
         uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
         const int dalign = (int)((uintptr_t)dst & 15u);
         uint8_t* dbase = dst - dalign;
         // ---- the payload stream
         uint32_t acc = 0;
-        stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen));
+        stream_row<U, NT, P>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen), part);
 #ifdef WGCS_GSO_STAMPS
         stp[2] = __builtin_amdgcn_s_memrealtime();
 #endif
-        finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
-                   tflags, id0, seq0, &sizes[slot0 + (uint32_t)i]);
+        // the parts' sums, lane by lane, into every row of the segment
+        if (P >= 2) acc += (uint32_t)__shfl_xor((int)acc, 16);  // a segment's u16 word sum stays < 2^31
+        if (P >= 4) acc += (uint32_t)__shfl_xor((int)acc, 32);
+        if (part == 0)
+          finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
+                     tflags, id0, seq0, &sizes[slot0 + (uint32_t)i]);
 #ifdef WGCS_GSO_STAMPS
         stp[3] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1051,7 +1079,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
     }
 #endif
   } else {
-    for (int grp = (int)blockIdx.y; group_live(grp); grp += (int)gridDim.y) {  // block-uniform
+    for (int grp = (int)blockIdx.y; group_live16(grp); grp += (int)gridDim.y) {  // block-uniform
       const int i = grp * ROWS + wv * 4 + (lane >> 4);
       uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
       const int live = decoded_rows<U, NT>(vb, jlen, job.flags, room, max_segs, i, grp == 0, &count[jb], &status[jb],
@@ -1072,9 +1100,11 @@ hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs
   if (!outpos) room = out_stride > offset ? out_stride - offset : 0;
   // 16 segments (4 waves) per block and group; a few blocks per job, each
   // looping over its groups (a 65,535-B read at MSS 1460 has 3 groups)
-  const uint32_t ngroups = (max_segs + 15) / 16;
-  const uint32_t gy = ngroups < (uint32_t)WGCS_GSO_GROUPS ? ngroups : (uint32_t)WGCS_GSO_GROUPS;
-  hipLaunchKernelGGL((gso_rows_kernel<WGCS_GSO_U, true>), dim3(n_jobs, gy), dim3(256), 0, s, arena, jobs, max_segs, out,
+  constexpr uint32_t segs = 16 / WGCS_GSO_PARTS, gmax = WGCS_GSO_GROUPS * WGCS_GSO_PARTS;
+  const uint32_t ngroups = (max_segs + segs - 1) / segs;
+  const uint32_t gy = ngroups < gmax ? ngroups : gmax;
+  hipLaunchKernelGGL((gso_rows_kernel<WGCS_GSO_U / WGCS_GSO_PARTS + (WGCS_GSO_PARTS == 4), true>), dim3(n_jobs, gy),
+                     dim3(256), 0, s, arena, jobs, max_segs, out,
                      out_stride, outpos, offset, room, sizes, count, status);
   return hipGetLastError();
 }
