@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--verify", action="store_true", help="check the GPU results against the synth ground truth")
     ap.add_argument("--no-strong", action="store_true",
                     help="cfg2: skip the configs[4] block (the 1M mixed batch split over the ranks, `cfg5_strong`)")
+    ap.add_argument("--no-gate", action="store_true",
+                    help="enqueue the K steps inside the timed region instead of posting them behind a doorbell")
     ap.add_argument("--no-affinity", action="store_true", help="do not bind each rank to its GPU's NUMA-local CPUs")
     ap.add_argument("--repeat", type=int, default=1,
                     help="diagnostics: time the K-step region this many times; `value` stays the FIRST region, "
@@ -196,7 +198,7 @@ def main():
     bytes_per_step = int(pkts_np["len"].astype(np.int64).sum())
     use_events = not args.no_event_timing
     leg = checksum_leg(torch, dev, arena_np, pkts_np, mode, args.steps, args.warmup, args.streams, args.rotate,
-                       barrier, use_events, repeat=args.repeat, verify=args.verify)
+                       barrier, use_events, repeat=args.repeat, verify=args.verify, gate=not args.no_gate)
     local_elapsed, kern_ms, iso_ms, S, R = leg["elapsed"], leg["kern_ms"], leg["iso_ms"], leg["streams"], leg["R"]
     elapsed = shard.max_over_ranks(local_elapsed, dist, device=red_dev)
     kern_all = shard.gather_floats(kern_ms if kern_ms is not None else -1.0, dist, device=red_dev)
@@ -245,7 +247,9 @@ def main():
         # first-launch latency + the completion wait (this rank; `value` uses the max over ranks)
         result["timing"] = {"wall_us": round(local_elapsed * 1e6, 2), "event_span_us": round(kern_ms * args.steps * 1e3, 2),
                             "wall_minus_span_us": round((local_elapsed - kern_ms * args.steps * 1e-3) * 1e6, 2),
-                            "enqueue": "one wgcs_checksum_batches call for the K steps"}
+                            "enqueue": ("one wgcs_checksum_batches call for the K steps" +
+                                        ("" if args.no_gate else ", posted behind a doorbell (wgcs_stream_wait_flag) "
+                                         "rung when the clock starts"))}
         if leg["repeats"]:
             result["timing"]["repeats"] = [{"wall_us": round(w * 1e6, 1), "event_span_us": round(m * args.steps * 1e3, 1)}
                                            for w, m in leg["repeats"]]
@@ -358,7 +362,7 @@ def roofline(kname, bytes_per_step, flen, n, kern_ms, S, iso_ms, kern_all=None) 
 
 
 def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, rotate, barrier, use_events,
-                 repeat=1, verify=False, iso=True):
+                 repeat=1, verify=False, iso=True, gate=True):
     """Time `steps` checksum launches (one batch each, inputs resident in HBM)
     after `warmup` untimed ones.  Returns {elapsed (this rank's wall s),
     kern_ms (HIP events, GPU ms per launch), iso_ms (one-stream reference),
@@ -396,12 +400,29 @@ def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, ro
     e0.record(strm[0])  # torch creates the HIP events on their first record
     e1.record(strm[0])
 
+    # The doorbell (gate): the K launches are posted behind a device-side wait
+    # on a pinned flag (wgcs_stream_wait_flag) before the clock starts, and the
+    # clock starts when the host rings it -- as a receive ring posts batches
+    # ahead and releases them when due.  The timed region then holds the K
+    # launches' GPU work and the completion wait, not the host's enqueue calls.
+    bell = dev.host_alloc(64).view(np.uint32) if gate else None
+
     def timed(K, k0, ns):
         bl = batches(K, k0)  # the step list (pointers only) is built before the clock starts
         barrier()
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        dev.checksum_batches(mode, bl, strm[:ns], e0 if use_events else None, e1 if use_events else None)
+        evs = (e0 if use_events else None, e1 if use_events else None)
+        if bell is not None:
+            bell[0] = 0
+            dev.stream_wait_flag(strm[0], bell, 1)  # streams[1:] wait on e0, recorded behind it
+            try:
+                dev.checksum_batches(mode, bl, strm[:ns], *evs)
+            finally:
+                t0 = time.perf_counter()
+                bell[0] = 1  # ring: never leave the streams gated
+        else:
+            t0 = time.perf_counter()
+            dev.checksum_batches(mode, bl, strm[:ns], *evs)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0  # the closing barrier is not timed: max over ranks covers skew
         barrier()
@@ -454,7 +475,7 @@ def strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_
     arena_np, pkts_np, _, lo, hi = shard.make_global_shard(n_cfg, rank, world, flen, kinds)
     bytes_rank = int(pkts_np["len"].astype(np.int64).sum())
     leg = checksum_leg(torch, dev, arena_np, pkts_np, mode, args.steps, args.warmup, 1, 2, barrier, use_events,
-                       iso=False)
+                       iso=False, gate=not args.no_gate)
     del arena_np
     elapsed = shard.max_over_ranks(leg["elapsed"], dist, device=red_dev)
     kern_all = shard.gather_floats(leg["kern_ms"] if leg["kern_ms"] is not None else -1.0, dist, device=red_dev)

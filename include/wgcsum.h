@@ -189,6 +189,14 @@ int wgcs_checksum_batches(wgcs_ctx *ctx, int mode, unsigned flags, const wgcs_ba
                           uint32_t n_batches, void *const *streams, uint32_t n_streams,
                           void *ev_begin, void *ev_end);
 
+/* A doorbell: work enqueued on `stream` (NULL: the context's) after this call
+ * starts only once *flag == value.  `flag` is a 4-byte-aligned word of
+ * wgcs_host_alloc memory (the device polls it); the host rings it with a plain
+ * store.  A receive / send ring posts its batches ahead of time and rings once
+ * they are due, so no host enqueue cost sits between a batch being ready and
+ * its launch.  The caller must ring before it waits on the stream. */
+int wgcs_stream_wait_flag(wgcs_ctx *ctx, void *stream, const uint32_t *flag, uint32_t value);
+
 /* gsoSplit for n_jobs super-packets.  Job j writes its segments into output
  * slots [j*max_segs, (j+1)*max_segs), slot s at d_out + s*out_stride + offset
  * (like bufs[s][offset:]).  d_sizes[slot] = packet size; d_count[j] = the

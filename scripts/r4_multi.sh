@@ -18,6 +18,17 @@ EOF
 cat $OUT/pci_probe.txt
 step drv1 300 python bench.py --gpus 1 --steps 20 --warmup 5
 grep '^{' $OUT/drv1.log > $OUT/drv1.jsonl
+# doorbell A/B on the driver's command shape (cfg2 only, interleaved)
+for r in 1 2 3; do
+  for g in gate nogate; do
+    extra=""; [ $g = nogate ] && extra="--no-gate"
+    step ab_${g}_$r 120 python bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --no-e2e --no-strong $extra && grep '^{' $OUT/ab_${g}_$r.log | sed "s/^{/{\"ab\": \"$g\", /" >> $OUT/gate_ab.jsonl
+  done
+done
+python3 -c "
+import json
+for l in open('$OUT/gate_ab.jsonl'):
+    d = json.loads(l); print(d['ab'], d['value'], d['timing']['wall_minus_span_us'], d['roofline']['kernel_ms'])"
 export WGCS_DIST_BACKEND=gloo
 step g2 300 python bench.py --gpus 2 --steps 20 --warmup 5
 grep '^{' $OUT/g2.log > $OUT/r4_rehearse_gpus2_gloo.jsonl

@@ -168,3 +168,42 @@ def test_empty_calls_return_nothing(dev):
     ws.wait(b)
     assert ws.result(b, i, 0) == (None, [], [])
     ws.close()
+
+
+def test_stream_wait_flag_doorbell(dev):
+    """wgcs_stream_wait_flag: a batch posted behind the doorbell does not run
+    until the host rings it, then runs exactly as an ungated one (bench.py
+    posts its timed steps this way).  Non-mapped flags are refused."""
+    import time
+
+    import torch
+
+    import oracle
+    from wireguard_amd import synth
+    from wireguard_amd.tun import MODE_VALIDATE
+
+    arena, pkts, _ = synth.make_batch(512, 1500, kinds="mixed")
+    d_arena = torch.from_numpy(arena).cuda()
+    d_pkts = torch.from_numpy(pkts.view(np.uint8)).cuda()
+    d_out = torch.full((512,), 7, dtype=torch.uint8, device="cuda")
+    bell = dev.host_alloc(64).view(np.uint32)
+    with pytest.raises(WgcsError):
+        dev.stream_wait_flag(None, np.zeros(4, np.uint32), 1)  # pageable memory
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    bell[0] = 0
+    dev.stream_wait_flag(s, bell, 1)
+    dev.checksum_batch(MODE_VALIDATE, d_arena, d_pkts, 512, d_out, stream=s)
+    ev = torch.cuda.Event()
+    ev.record(s)
+    time.sleep(0.05)
+    gated = not ev.query()
+    bell[0] = 1  # ring (always, before any wait on the stream)
+    t0 = time.time()
+    while not ev.query():
+        assert time.time() - t0 < 10, "doorbell never released the stream"
+        time.sleep(0.001)
+    assert gated, "the batch ran before the doorbell was rung"
+    want = oracle.checksum_batch(MODE_VALIDATE, arena, pkts)
+    assert np.array_equal(d_out.cpu().numpy(), want) and want.all()
+    dev.host_free(bell.view(np.uint8))

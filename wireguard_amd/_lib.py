@@ -128,6 +128,7 @@ def load() -> C.CDLL:
         "wgcs_wstager_submit": ([vp, C.POINTER(u64)], i32),
         "wgcs_host_alloc": ([vp, sz, C.POINTER(vp)], i32),
         "wgcs_host_free": ([vp, vp], i32),
+        "wgcs_stream_wait_flag": ([vp, vp, vp, u32], i32),
         "wgcs_wstager_wait": ([vp, u64], i32),
         "wgcs_wstager_result": ([vp, u64, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(vp),
                                  C.POINTER(sz)], i32),

@@ -314,6 +314,17 @@ int wgcs_checksum_batches(wgcs_ctx* ctx, int mode, unsigned flags, const wgcs_ba
   return WGCS_OK;
 }
 
+int wgcs_stream_wait_flag(wgcs_ctx* ctx, void* stream, const uint32_t* flag, uint32_t value) {
+  if (!ctx || !flag || ((uintptr_t)flag & 3u)) return WGCS_ERR_INVALID_ARG;
+  if (!host_mapped(ctx, flag, sizeof(uint32_t)))
+    return set_err(ctx, WGCS_ERR_INVALID_ARG, "wgcs_stream_wait_flag: flag is not wgcs_host_alloc memory");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  const hipError_t e = hipStreamWaitValue32(s, const_cast<uint32_t*>(flag), value, hipStreamWaitValueEq, 0xFFFFFFFFu);
+  return e == hipSuccess ? WGCS_OK : hip_fail(ctx, e, "hipStreamWaitValue32");
+}
+
 // Host batches up to this size run zero-copy (the kernel reads pinned staging
 // over PCIe); larger ones go through copy-engine H2D / D2H.
 constexpr size_t kZeroCopyMax = 1u << 20;

@@ -147,6 +147,13 @@ class Device:
     def host_free(self, arr: np.ndarray) -> None:
         self._check(self.lib.wgcs_host_free(self.h, arr.ctypes.data))
 
+    def stream_wait_flag(self, stream, flag: np.ndarray, value: int = 1) -> None:
+        """wgcs_stream_wait_flag: work enqueued on `stream` afterwards waits
+        until flag[0] == value (flag: a uint32 view of host_alloc memory);
+        the host rings it with `flag[0] = value`."""
+        s = getattr(stream, "cuda_stream", stream)
+        self._check(self.lib.wgcs_stream_wait_flag(self.h, s, flag.ctypes.data, value))
+
     # ---------------------------------------------------------- device batch
     def checksum_batch(self, mode: int, arena, pkts, n: int, out, initial=None, inplace: bool = False,
                        stream=None) -> None:
