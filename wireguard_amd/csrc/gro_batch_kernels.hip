@@ -525,6 +525,10 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
                                                         int32_t* __restrict__ status, int32_t* __restrict__ n_write,
                                                         int32_t* __restrict__ to_write) {
   __shared__ GroSmem S;
+#ifdef WGCS_GRO_STAMPS  // timing-only build (scripts/probe_gro_phases.py): s_memrealtime at each phase boundary
+  uint64_t stp[6];
+  stp[0] = __builtin_amdgcn_s_memrealtime();
+#endif
   const int t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6, r = lane & 15, row = t >> 4;
   const wgcs_gro_call call = calls[blockIdx.x];
@@ -679,6 +683,9 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
   }
   __syncthreads();
 
+#ifdef WGCS_GRO_STAMPS
+  stp[1] = __builtin_amdgcn_s_memrealtime();
+#endif
   // ---- 2. flow ids (first earlier packet with the same key in the same table)
   if (t < n_eff && S.cand[t] != C_NOT && !S.noop[t]) {
     const uint8_t c = S.cand[t];
@@ -722,6 +729,9 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
   }
   __syncthreads();
 
+#ifdef WGCS_GRO_STAMPS
+  stp[2] = __builtin_amdgcn_s_memrealtime();
+#endif
   // ---- 3. the handleGRO loop: one thread per flow.  First each packet's
   // PktRec -- {seq, ipattr, gsoSize | fnext << 16, th | iph << 8 | psh << 16 |
   // valid << 24} -- over the dead key words, so the walker fetches a packet
@@ -738,6 +748,9 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
   Planner P{S, arena, offset};
   if (live && S.flow[t] == t) P.run_flow(t);
   __syncthreads();
+#ifdef WGCS_GRO_STAMPS
+  stp[3] = __builtin_amdgcn_s_memrealtime();
+#endif
   // toWrite in packet order (groResultNoop and groResultTableInsert,
   // gro.go:1349-1362); NOOP buffers get an empty virtioNetHdr (:1350-1358)
   if (wv == 0) {
@@ -755,6 +768,9 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
   if (t < n_eff && S.it_alive[t]) P.finish_item(t, raw);
   __syncthreads();
 
+#ifdef WGCS_GRO_STAMPS
+  stp[4] = __builtin_amdgcn_s_memrealtime();
+#endif
   // ---- 4. apply in place
   // slice headers after the prepend swaps; toWrite; status
   if (t < n) {
@@ -840,6 +856,12 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
       head[lane - kVnet] = (uint8_t)vb;
     }
   }
+#ifdef WGCS_GRO_STAMPS  // to_write[first + 100 .. 106) of 128-buffer calls with < 100 writes (the bench's shapes)
+  __syncthreads();
+  stp[5] = __builtin_amdgcn_s_memrealtime();
+  if (t == 0 && n == kMaxB && S.n_write < 100)
+    for (int k = 0; k < 6; ++k) to_write[call.first + 100 + k] = (int32_t)(uint32_t)stp[k];
+#endif
 }
 
 // ---- write stager (wstager.cpp): staged packets -> slices, toWrite images -> packed output
