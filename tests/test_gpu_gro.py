@@ -168,3 +168,13 @@ def test_tcp_options_host_path(dev):
         pk = fa + fb + flow(4, seed=300 + k)
         order = np.argsort(rng.random(len(pk)) * (2.0 if k > 2 else 0.2) + np.arange(len(pk)) * 0.1)
         run_both(dev, [pk[i] for i in order])
+
+
+def test_quirk_calls_host_path(dev):
+    """The integer-width / PSH quirk calls (test_gpu_gro_batch.quirk_calls:
+    capacities above 64 KiB, a mid-flow PSH, sequence numbers wrapping 2^32)
+    through the per-call host path (wgcs_handle_gro)."""
+    from test_gpu_gro_batch import quirk_calls
+
+    for pkts, cap, can_udp, lo in quirk_calls():
+        run_both(dev, pkts, cap=cap, can_udp=can_udp, lens_override=lo)

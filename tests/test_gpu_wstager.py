@@ -351,3 +351,26 @@ def test_host_free_refused_while_a_slot_reads_it(dev):
     assert (0 if err is None else err.code, tw_p, writes_p) == (rc, tw, writes)
     dev.host_free(pool)
     ws.close()
+
+
+def test_write_stager_quirk_calls(dev):
+    """The quirk calls (capacities above 64 KiB: items and their uint16 length
+    fields grow past 65,535; a mid-flow PSH; sequence numbers wrapping) through
+    the write stager, every write(2) image vs the oracle."""
+    from test_gpu_gro_batch import quirk_calls
+
+    calls = quirk_calls()
+    ws = WriteStager(dev, depth=2, max_writes=16, max_pkts=16 * 128, max_bytes=16 * 128 * 1600)
+    keep, idxs = [], []
+    for pkts, cap, can_udp, lo in calls:
+        bufs, lens = _mk(pkts, cap, OFFSET, lo)
+        keep.append(bufs)
+        idxs.append(ws.push(bufs, lens, OFFSET, can_udp))
+    b = ws.submit()
+    ws.wait(b)
+    for k, (pkts, cap, can_udp, lo) in enumerate(calls):
+        rc, tw, writes = _oracle_writes(pkts, cap, can_udp, OFFSET, lo)
+        err, tw_p, writes_p = ws.result(b, idxs[k], len(pkts))
+        assert (0 if err is None else err.code, tw_p) == (rc, tw), k
+        assert writes_p == writes, f"call {k}: {_first_diff(writes_p, writes)}"
+    ws.close()

@@ -499,7 +499,7 @@ __device__ void row_copy(const uint8_t* src, int n, uint8_t* dst, int r) {
 __device__ __forceinline__ uint32_t patched(uint32_t b, int x, int iphl, int csum_at, uint32_t pkt_len, bool v6,
                                             bool udp, bool pshf) {
   if (!v6) {
-    if (x == 2) b = pkt_len >> 8;  // total length (:1131 / :1214)
+    if (x == 2) b = (pkt_len >> 8) & 0xFF;  // total length, uint16(len(pkt)) (:1131 / :1214)
     if (x == 3) b = pkt_len & 0xFF;
     if (x == 10 || x == 11) b = 0;  // :1134 / :1217
   } else {

@@ -34,7 +34,7 @@ struct HdrPatch {
 __device__ __forceinline__ uint32_t patched(const uint8_t* head, const HdrPatch& h, int x) {
   uint32_t b = head[x];
   if (!h.v6) {
-    if (x == 2) b = h.pkt_len >> 8;  // total length (gro.go:1131 / :1214)
+    if (x == 2) b = (h.pkt_len >> 8) & 0xFF;  // total length, uint16(len(pkt)) (gro.go:1131 / :1214)
     if (x == 3) b = h.pkt_len & 0xFF;
     if (x == 10 || x == 11) b = 0;   // :1134 / :1217
   } else {
