@@ -532,59 +532,78 @@ __device__ __forceinline__ void load_windows(__amdgpu_buffer_rsrc_t rs, int aoff
 // Wave-uniform: no lane of the wave has `pred` set (a scalar compare, no exec-mask branch).
 __device__ __forceinline__ bool wave_none(bool pred) { return __builtin_amdgcn_ballot_w64(pred) == 0; }
 
-// One row's payload stream: destination chunk k = bytes [sb, sb + 16) of the
-// dword-aligned source window k and the first dword of window k + 1 (next
-// lane, DPP row_ror).  Sums the L4 bytes [hdrLen, pktLen) from the same
+// A row's source geometry for segment i: the dword-aligned window of its
+// destination chunk 0 (job-relative offset aoff, byte shift sb), the job
+// bytes [lo, hi) of its payload, its chunk count nk and packet length.
+struct RowSrc {
+  int aoff, sb, lo, hi, nk, pkt_len;
+};
+__device__ __forceinline__ RowSrc row_src(const uint8_t* rb, int i, int gso, int hdr_len, int plen, int dalign) {
+  RowSrc g;
+  const int seg_start = hdr_len + i * gso;
+  const int seg_end = min(plen, seg_start + gso);
+  g.pkt_len = hdr_len + (seg_end - seg_start);
+  g.nk = (g.pkt_len + dalign + 15) >> 4;
+  const uint8_t* w0 = rb + (int64_t)i * gso - dalign;  // source of destination chunk 0 (payload positions)
+  g.sb = (int)((uintptr_t)w0 & 3u);
+  g.aoff = (int)(w0 - g.sb - (rb - 10));               // its dword-aligned window, job-relative
+  g.lo = 10 + seg_start;
+  g.hi = 10 + seg_end;
+  return g;
+}
+
+// One batch of a row's payload stream: destination chunk k = bytes [sb, sb +
+// 16) of the dword-aligned source window k and the first dword of window k + 1
+// (next lane, DPP row_ror).  Sums the L4 bytes [hdrLen, pktLen) from the same
 // registers (v_dot2) and stores the payload bytes of every chunk (those of a
 // chunk shared with the header as byte-exact pieces; the header phase stores
 // the chunk's header bytes).
-// A segment may be split over P rows (part = 0 .. P-1): part p takes the
-// batches of 16 * U chunks starting at p, p + P, ... (P = 1: the whole segment).
-template <int U, bool NT, int P = 1>
+template <int U>
+__device__ __forceinline__ void consume_batch(const uint4 (&A)[U], uint32_t E, int k0, const RowSrc& g, int hdr_len,
+                                              int dalign, uint8_t* dbase, int r, uint32_t& acc) {
+  const int pkt_len = g.pkt_len, nk = g.nk, sb = g.sb;
+  uint32_t Rc = row_next(A[0].x);  // lane 15: lane 0's next-u dword
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int k = k0 + r + 16 * u;
+    const uint32_t Rx = u + 1 < U ? row_next(A[u + 1 < U ? u + 1 : u].x) : E;
+    const uint32_t nx = r == 15 ? Rx : Rc;
+    Rc = Rx;
+    const int x0 = 16 * k - dalign;
+    const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(A[u].y, A[u].x, sb),
+                               __builtin_amdgcn_alignbyte(A[u].z, A[u].y, sb),
+                               __builtin_amdgcn_alignbyte(A[u].w, A[u].z, sb),
+                               __builtin_amdgcn_alignbyte(nx, A[u].w, sb));
+    if (wave_none(x0 < hdr_len || x0 + 16 > pkt_len)) {
+      // every chunk of this step in every row of the wave is whole payload
+      // (the bulk of a segment): unmasked sum and a full store, no branches
+      acc = add4(acc, v);
+      int ko = 16 * k;
+      asm volatile("" : "+v"(ko));
+      *reinterpret_cast<uint4*>(dbase + ko) = v;
+    } else if (k < nk) {
+      if (x0 >= hdr_len && x0 + 16 <= pkt_len) acc = add4(acc, v);
+      else acc = add4_masked(acc, v, byte_bits16(hdr_len - x0, pkt_len - x0), false);
+      // the chunk's address formed here, not hoisted for all U chunks up front
+      // (six 64-bit addresses held across the stream cost an occupancy step)
+      int ko = 16 * k;
+      asm volatile("" : "+v"(ko));
+      store_chunk(dbase + ko, v, x0 - hdr_len, pkt_len - hdr_len);  // bytes [hdrLen, pktLen)
+    }
+  }
+}
+
+// One row's whole payload stream, batch by batch.
+template <int U, bool NT>
 __device__ __forceinline__ void stream_row(const uint8_t* rb, int i, int gso, int hdr_len, int plen, int dalign,
-                                           uint8_t* dbase, int r, uint32_t& acc, __amdgpu_buffer_rsrc_t rs,
-                                           int part = 0) {
-  const int seg_start = hdr_len + i * gso;
-  const int seg_end = min(plen, seg_start + gso);
-  const int pkt_len = hdr_len + (seg_end - seg_start);
-  const int nk = (pkt_len + dalign + 15) >> 4;
-  const uint8_t* w0 = rb + (int64_t)i * gso - dalign;  // source of destination chunk 0 (payload positions)
-  const int sb = (int)((uintptr_t)w0 & 3u);
-  const int aoff = (int)(w0 - sb - (rb - 10));         // its dword-aligned window, job-relative
+                                           uint8_t* dbase, int r, uint32_t& acc, __amdgpu_buffer_rsrc_t rs) {
+  const RowSrc g = row_src(rb, i, gso, hdr_len, plen, dalign);
   acc = 0;
-  for (int k0 = 16 * U * part; k0 < nk; k0 += 16 * U * P) {
+  for (int k0 = 0; k0 < g.nk; k0 += 16 * U) {
     uint4 A[U];
     uint32_t E;
-    load_windows<U, NT>(rs, aoff, k0, r, 10 + seg_start, 10 + seg_end, A, E);
-    uint32_t Rc = row_next(A[0].x);  // lane 15: lane 0's next-u dword
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = k0 + r + 16 * u;
-      const uint32_t Rx = u + 1 < U ? row_next(A[u + 1 < U ? u + 1 : u].x) : E;
-      const uint32_t nx = r == 15 ? Rx : Rc;
-      Rc = Rx;
-      const int x0 = 16 * k - dalign;
-      const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(A[u].y, A[u].x, sb),
-                                 __builtin_amdgcn_alignbyte(A[u].z, A[u].y, sb),
-                                 __builtin_amdgcn_alignbyte(A[u].w, A[u].z, sb),
-                                 __builtin_amdgcn_alignbyte(nx, A[u].w, sb));
-      if (wave_none(x0 < hdr_len || x0 + 16 > pkt_len)) {
-        // every chunk of this step in every row of the wave is whole payload
-        // (the bulk of a segment): unmasked sum and a full store, no branches
-        acc = add4(acc, v);
-        int ko = 16 * k;
-        asm volatile("" : "+v"(ko));
-        *reinterpret_cast<uint4*>(dbase + ko) = v;
-      } else if (k < nk) {
-        if (x0 >= hdr_len && x0 + 16 <= pkt_len) acc = add4(acc, v);
-        else acc = add4_masked(acc, v, byte_bits16(hdr_len - x0, pkt_len - x0), false);
-        // the chunk's address formed here, not hoisted for all U chunks up front
-        // (six 64-bit addresses held across the stream cost an occupancy step)
-        int ko = 16 * k;
-        asm volatile("" : "+v"(ko));
-        store_chunk(dbase + ko, v, x0 - hdr_len, pkt_len - hdr_len);  // bytes [hdrLen, pktLen)
-      }
-    }
+    load_windows<U, NT>(rs, g.aoff, k0, r, g.lo, g.hi, A, E);
+    consume_batch<U>(A, E, k0, g, hdr_len, dalign, dbase, r, acc);
   }
 }
 
@@ -861,18 +880,17 @@ __device__ __noinline__ int decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, u
 #ifndef WGCS_GSO_WAVES
 #define WGCS_GSO_WAVES 5
 #endif
+// Segments per row on the clean path: 2 = each row takes segments i and i +
+// 16 of a 32-segment group and issues both segments' payload loads before it
+// consumes the first, so half the waves (and heads) carry the same bytes in
+// flight and the first segment's stores overlap the second's loads.  Used when
+// a segment fits one batch of windows (hdrLen + gsoSize <= 16 * 16 * U - 30).
+#ifndef WGCS_GSO_ROWSEGS
+#define WGCS_GSO_ROWSEGS 1
+#endif
 #ifndef WGCS_GSO_GROUPS
-#define WGCS_GSO_GROUPS 3  // blocks per job (grid y) at one row per segment; each takes every WGCS_GSO_GROUPS-th group
+#define WGCS_GSO_GROUPS (WGCS_GSO_ROWSEGS == 2 ? 2 : 3)  // blocks per job (grid y); each takes every GROUPS-th group
 #endif
-// Rows per segment on the clean path (1, 2 or 4): P rows share one segment's
-// payload stream (part p: chunk batches p, p + P, ...), so a block's 16 rows
-// hold 16 / P segments and a job needs P times the waves -- more, shorter
-// waves per launch.  The part sums meet in part 0's row (lane-wise, across
-// rows), which writes the header chunk, the checksums and the size.
-#ifndef WGCS_GSO_PARTS
-#define WGCS_GSO_PARTS 1
-#endif
-static_assert(WGCS_GSO_PARTS == 1 || WGCS_GSO_PARTS == 2 || WGCS_GSO_PARTS == 4, "WGCS_GSO_PARTS: 1, 2 or 4");
 template <int U, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WAVES, 8))) void gso_rows_kernel(const uint8_t* __restrict__ arena,
                                                        const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
@@ -880,9 +898,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
                                                        const GsoOutPos* __restrict__ outpos, uint32_t offset,
                                                        uint32_t room, int32_t* __restrict__ sizes,
                                                        int32_t* __restrict__ count, int32_t* __restrict__ status) {
-  constexpr int ROWS = 16;                    // rows per block; segments per group on the decoded path
-  constexpr int P = WGCS_GSO_PARTS;
-  constexpr int SEGS = ROWS / P;              // segments per group on the clean path
+  constexpr int ROWS = 16;
 #ifdef WGCS_GSO_STAMPS  // timing-only build (scripts/probe_gso_stamps.py): s_memrealtime per wave phase
   uint64_t stp[5] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0};
 #endif
@@ -964,21 +980,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   // Groups that may hold a segment: gbound = max(1, min(ngroups, ceil(nbound /
   // 16))) with nbound = ceil((plen - hmin) / gsoSize); group y < gbound iff y
   // == 0 or (y < ngroups and 16 y gsoSize < plen - hmin).
-  const int ngroups = (int)((max_segs + SEGS - 1) / SEGS);
+  const int ngroups = (int)((max_segs + ROWS - 1) / ROWS);
   const int hmin = raw ? (int)hl : (tcp_s ? cs_s + 20 : cs_s + 8);
   const bool split_type = jlen >= 14 && ok_s && cs_s + 60 <= 0xFFFF;
   const bool gso_none = jlen >= 14 && !raw && t1 == GSO_NONE;
   auto group_live = [&](int y) {
     if (y == 0) return true;
     if (gso_none || y >= ngroups) return false;
-    return !split_type || (plen_s > hmin && hmin + (int64_t)y * SEGS * gso_s < plen_s);
-  };
-  // the decoded path keeps one row per segment: groups of ROWS segments
-  // (a block live for them is live for the clean path's groups of SEGS)
-  const int ngroups16 = (int)((max_segs + ROWS - 1) / ROWS);
-  auto group_live16 = [&](int y) {
-    if (y == 0) return true;
-    if (gso_none || y >= ngroups16) return false;
     return !split_type || (plen_s > hmin && hmin + (int64_t)y * ROWS * gso_s < plen_s);
   };
   if (!group_live((int)blockIdx.y)) return;
@@ -1045,26 +1053,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
     if (ufl((int)(ip_base + l4_base + tflags + id0 + seq0)) == 0x7FFFFFFF) sizes[slot0] = 0;
     return;
 #endif
-    for (int grp = (int)blockIdx.y; has_seg(grp * SEGS); grp += (int)gridDim.y) {  // block-uniform
-      const int row = wv * 4 + (lane >> 4);
-      const int i = grp * SEGS + row / P;  // this row's segment
-      const int part = row % P;            // and its part of it
-      if (has_seg(i)) {  // row-uniform (the P rows of a segment agree)
+    // both segments of a row in one batch of windows each (wave-uniform)
+    const bool pair = WGCS_GSO_ROWSEGS == 2 && hdr_len + gso + 30 <= 16 * 16 * U;
+    if (pair) {
+      const __amdgpu_buffer_rsrc_t rs = job_rsrc(vb, jlen);
+      for (int grp = (int)blockIdx.y; has_seg(grp * 2 * ROWS); grp += (int)gridDim.y) {  // block-uniform
+        const int i0 = grp * 2 * ROWS + wv * 4 + (lane >> 4), i1 = i0 + ROWS;
+        const bool h0 = has_seg(i0), h1 = has_seg(i1);  // row-uniform
+        uint8_t* dst0 = out + obase + (uint64_t)i0 * opitch + offset;
+        uint8_t* dst1 = out + obase + (uint64_t)i1 * opitch + offset;
+        const int da0 = (int)((uintptr_t)dst0 & 15u), da1 = (int)((uintptr_t)dst1 & 15u);
+        const RowSrc g0 = row_src(rb, i0, gso, hdr_len, plen, da0), g1 = row_src(rb, i1, gso, hdr_len, plen, da1);
+        // both segments' windows in flight (a row without the segment: an
+        // empty byte range, every window past the resource, no memory touched)
+        uint4 A0[U], A1[U];
+        uint32_t E0, E1;
+        load_windows<U, NT>(rs, g0.aoff, 0, r, h0 ? g0.lo : 0, h0 ? g0.hi : 0, A0, E0);
+        load_windows<U, NT>(rs, g1.aoff, 0, r, h1 ? g1.lo : 0, h1 ? g1.hi : 0, A1, E1);
+        if (h0) {
+          uint32_t acc = 0;
+          consume_batch<U>(A0, E0, 0, g0, hdr_len, da0, dst0 - da0, r, acc);
+          finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i0, r, da0, dst0, dst0 - da0, acc, ip_base,
+                     l4_base, tflags, id0, seq0, &sizes[slot0 + (uint32_t)i0]);
+        }
+        if (h1) {
+          uint32_t acc = 0;
+          consume_batch<U>(A1, E1, 0, g1, hdr_len, da1, dst1 - da1, r, acc);
+          finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i1, r, da1, dst1, dst1 - da1, acc, ip_base,
+                     l4_base, tflags, id0, seq0, &sizes[slot0 + (uint32_t)i1]);
+        }
+      }
+    } else
+    for (int grp = (int)blockIdx.y; has_seg(grp * ROWS); grp += (int)gridDim.y) {  // block-uniform
+      const int i = grp * ROWS + wv * 4 + (lane >> 4);  // this row's segment
+      if (has_seg(i)) {  // row-uniform
         uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
         const int dalign = (int)((uintptr_t)dst & 15u);
         uint8_t* dbase = dst - dalign;
         // ---- the payload stream
         uint32_t acc = 0;
-        stream_row<U, NT, P>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen), part);
+        stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen));
 #ifdef WGCS_GSO_STAMPS
         stp[2] = __builtin_amdgcn_s_memrealtime();
 #endif
-        // the parts' sums, lane by lane, into every row of the segment
-        if (P >= 2) acc += (uint32_t)__shfl_xor((int)acc, 16);  // a segment's u16 word sum stays < 2^31
-        if (P >= 4) acc += (uint32_t)__shfl_xor((int)acc, 32);
-        if (part == 0)
-          finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
-                     tflags, id0, seq0, &sizes[slot0 + (uint32_t)i]);
+        finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
+                   tflags, id0, seq0, &sizes[slot0 + (uint32_t)i]);
 #ifdef WGCS_GSO_STAMPS
         stp[3] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1079,7 +1112,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
     }
 #endif
   } else {
-    for (int grp = (int)blockIdx.y; group_live16(grp); grp += (int)gridDim.y) {  // block-uniform
+    for (int grp = (int)blockIdx.y; group_live(grp); grp += (int)gridDim.y) {  // block-uniform
       const int i = grp * ROWS + wv * 4 + (lane >> 4);
       uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
       const int live = decoded_rows<U, NT>(vb, jlen, job.flags, room, max_segs, i, grp == 0, &count[jb], &status[jb],
@@ -1100,11 +1133,9 @@ hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs
   if (!outpos) room = out_stride > offset ? out_stride - offset : 0;
   // 16 segments (4 waves) per block and group; a few blocks per job, each
   // looping over its groups (a 65,535-B read at MSS 1460 has 3 groups)
-  constexpr uint32_t segs = 16 / WGCS_GSO_PARTS, gmax = WGCS_GSO_GROUPS * WGCS_GSO_PARTS;
-  const uint32_t ngroups = (max_segs + segs - 1) / segs;
-  const uint32_t gy = ngroups < gmax ? ngroups : gmax;
-  hipLaunchKernelGGL((gso_rows_kernel<WGCS_GSO_U / WGCS_GSO_PARTS + (WGCS_GSO_PARTS == 4), true>), dim3(n_jobs, gy),
-                     dim3(256), 0, s, arena, jobs, max_segs, out,
+  const uint32_t ngroups = (max_segs + 16 * WGCS_GSO_ROWSEGS - 1) / (16 * WGCS_GSO_ROWSEGS);
+  const uint32_t gy = ngroups < (uint32_t)WGCS_GSO_GROUPS ? ngroups : (uint32_t)WGCS_GSO_GROUPS;
+  hipLaunchKernelGGL((gso_rows_kernel<WGCS_GSO_U, true>), dim3(n_jobs, gy), dim3(256), 0, s, arena, jobs, max_segs, out,
                      out_stride, outpos, offset, room, sizes, count, status);
   return hipGetLastError();
 }
