@@ -47,17 +47,18 @@ def test_launcher_command_runs_n_ranks(tmp_path):
     assert "--nproc-per-node=2" in cmd and "--master-addr=127.0.0.1" in cmd
     assert cmd[cmd.index(script) + 1:] == ["--gpus", "2", "--steps", "3"]
     stand_in = tmp_path / "rank.py"
+    # each rank reports into its own file: two ranks printing to one stdout may interleave
     stand_in.write_text(
         "import json, os, sys\n"
         "import torch.distributed as dist\n"
         "dist.init_process_group('gloo')\n"
-        "print(json.dumps({'rank': dist.get_rank(), 'world': dist.get_world_size(), 'argv': sys.argv[1:]}), "
-        "flush=True)\n"
+        f"open(os.path.join({str(tmp_path)!r}, 'rank%d.json' % dist.get_rank()), 'w').write(json.dumps("
+        "{'rank': dist.get_rank(), 'world': dist.get_world_size(), 'argv': sys.argv[1:]}))\n"
         "dist.barrier(); dist.destroy_process_group()\n")
     cmd[cmd.index(script)] = str(stand_in)
     r = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    lines = [json.loads((tmp_path / f"rank{k}.json").read_text()) for k in range(2)]
     assert sorted(l["rank"] for l in lines) == [0, 1]
     assert all(l["world"] == 2 and l["argv"] == ["--gpus", "2", "--steps", "3"] for l in lines)
 

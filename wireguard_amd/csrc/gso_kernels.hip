@@ -880,16 +880,8 @@ __device__ __noinline__ int decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, u
 #ifndef WGCS_GSO_WAVES
 #define WGCS_GSO_WAVES 5
 #endif
-// Segments per row on the clean path: 2 = each row takes segments i and i +
-// 16 of a 32-segment group and issues both segments' payload loads before it
-// consumes the first, so half the waves (and heads) carry the same bytes in
-// flight and the first segment's stores overlap the second's loads.  Used when
-// a segment fits one batch of windows (hdrLen + gsoSize <= 16 * 16 * U - 30).
-#ifndef WGCS_GSO_ROWSEGS
-#define WGCS_GSO_ROWSEGS 1
-#endif
 #ifndef WGCS_GSO_GROUPS
-#define WGCS_GSO_GROUPS (WGCS_GSO_ROWSEGS == 2 ? 2 : 3)  // blocks per job (grid y); each takes every GROUPS-th group
+#define WGCS_GSO_GROUPS 3  // blocks per job (grid y); each takes every WGCS_GSO_GROUPS-th segment group
 #endif
 template <int U, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WAVES, 8))) void gso_rows_kernel(const uint8_t* __restrict__ arena,
@@ -1053,37 +1045,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
     if (ufl((int)(ip_base + l4_base + tflags + id0 + seq0)) == 0x7FFFFFFF) sizes[slot0] = 0;
     return;
 #endif
-    // both segments of a row in one batch of windows each (wave-uniform)
-    const bool pair = WGCS_GSO_ROWSEGS == 2 && hdr_len + gso + 30 <= 16 * 16 * U;
-    if (pair) {
-      const __amdgpu_buffer_rsrc_t rs = job_rsrc(vb, jlen);
-      for (int grp = (int)blockIdx.y; has_seg(grp * 2 * ROWS); grp += (int)gridDim.y) {  // block-uniform
-        const int i0 = grp * 2 * ROWS + wv * 4 + (lane >> 4), i1 = i0 + ROWS;
-        const bool h0 = has_seg(i0), h1 = has_seg(i1);  // row-uniform
-        uint8_t* dst0 = out + obase + (uint64_t)i0 * opitch + offset;
-        uint8_t* dst1 = out + obase + (uint64_t)i1 * opitch + offset;
-        const int da0 = (int)((uintptr_t)dst0 & 15u), da1 = (int)((uintptr_t)dst1 & 15u);
-        const RowSrc g0 = row_src(rb, i0, gso, hdr_len, plen, da0), g1 = row_src(rb, i1, gso, hdr_len, plen, da1);
-        // both segments' windows in flight (a row without the segment: an
-        // empty byte range, every window past the resource, no memory touched)
-        uint4 A0[U], A1[U];
-        uint32_t E0, E1;
-        load_windows<U, NT>(rs, g0.aoff, 0, r, h0 ? g0.lo : 0, h0 ? g0.hi : 0, A0, E0);
-        load_windows<U, NT>(rs, g1.aoff, 0, r, h1 ? g1.lo : 0, h1 ? g1.hi : 0, A1, E1);
-        if (h0) {
-          uint32_t acc = 0;
-          consume_batch<U>(A0, E0, 0, g0, hdr_len, da0, dst0 - da0, r, acc);
-          finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i0, r, da0, dst0, dst0 - da0, acc, ip_base,
-                     l4_base, tflags, id0, seq0, &sizes[slot0 + (uint32_t)i0]);
-        }
-        if (h1) {
-          uint32_t acc = 0;
-          consume_batch<U>(A1, E1, 0, g1, hdr_len, da1, dst1 - da1, r, acc);
-          finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i1, r, da1, dst1, dst1 - da1, acc, ip_base,
-                     l4_base, tflags, id0, seq0, &sizes[slot0 + (uint32_t)i1]);
-        }
-      }
-    } else
     for (int grp = (int)blockIdx.y; has_seg(grp * ROWS); grp += (int)gridDim.y) {  // block-uniform
       const int i = grp * ROWS + wv * 4 + (lane >> 4);  // this row's segment
       if (has_seg(i)) {  // row-uniform
@@ -1133,7 +1094,7 @@ hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs
   if (!outpos) room = out_stride > offset ? out_stride - offset : 0;
   // 16 segments (4 waves) per block and group; a few blocks per job, each
   // looping over its groups (a 65,535-B read at MSS 1460 has 3 groups)
-  const uint32_t ngroups = (max_segs + 16 * WGCS_GSO_ROWSEGS - 1) / (16 * WGCS_GSO_ROWSEGS);
+  const uint32_t ngroups = (max_segs + 15) / 16;
   const uint32_t gy = ngroups < (uint32_t)WGCS_GSO_GROUPS ? ngroups : (uint32_t)WGCS_GSO_GROUPS;
   hipLaunchKernelGGL((gso_rows_kernel<WGCS_GSO_U, true>), dim3(n_jobs, gy), dim3(256), 0, s, arena, jobs, max_segs, out,
                      out_stride, outpos, offset, room, sizes, count, status);
