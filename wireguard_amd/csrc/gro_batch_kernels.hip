@@ -43,6 +43,7 @@ namespace {
 constexpr int kMaxB = WGCS_GRO_MAX_CALL;  // buffers per call (one per thread)
 constexpr int kNone = -1;
 constexpr int kVnet = 10;
+constexpr int kCoopMin = 8;  // packets of a TCP flow from which one wave walks it
 enum : uint8_t { C_NOT = 0, C_TCP4 = 1, C_TCP6 = 2, C_UDP4 = 3, C_UDP6 = 4 };
 enum { R_NOOP = 0, R_INSERT = 1, R_COALESCED = 2 };
 enum { CC_PREPEND = -1, CC_UNAV = 0, CC_APPEND = 1 };
@@ -73,7 +74,12 @@ struct GroSmem {
   uint8_t res[kMaxB];                   // groResult of each packet (R_*)
   int16_t ndst[kMaxB];                  // piece p's destination buffer in its final item (-1: none)
   uint32_t npos[kMaxB];                 // ... and its first byte there
-  int n_eff, n_write, n_mat;
+  // long TCP flows walked by a whole wave (Planner::run_flow_wave): the flow's
+  // packet count, its items as an array (fitem[fbase[f] .. fbase[f] + fnit[f])
+  // in insertion order), the list of such flows
+  uint32_t fsize[kMaxB];
+  int16_t fbase[kMaxB], fnit[kMaxB], fitem[kMaxB], coop[kMaxB];
+  int n_eff, n_write, n_mat, n_coop, fitem_top;
 };
 
 __device__ __forceinline__ uint32_t be16g(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
@@ -93,6 +99,16 @@ struct Planner {
 
   __device__ void insert(int bi, int f, uint8_t bad) {  // tcpGROTable.insert / udpGROTable.insert
     const int it = bi;  // an item is named after the packet that inserted it
+    init_item(bi, bad);
+    S.it_next[it] = kNone;
+    S.it_prev[it] = S.fl_tail[f];
+    if (S.fl_tail[f] != kNone) S.it_next[S.fl_tail[f]] = (int16_t)it;
+    else S.fl_head[f] = (int16_t)it;
+    S.fl_tail[f] = (int16_t)it;
+  }
+
+  __device__ void init_item(int bi, uint8_t bad) {  // the new item's fields (gro.go:216-225, :358-364)
+    const int it = bi;
     S.it_slot[it] = (int16_t)bi;
     S.it_seq[it] = S.seq[bi];
     S.it_nm[it] = 0;
@@ -103,11 +119,6 @@ struct Planner {
     S.it_bad[it] = bad;
     S.it_alive[it] = 1;
     S.it_cand[it] = S.cand[bi];
-    S.it_next[it] = kNone;
-    S.it_prev[it] = S.fl_tail[f];
-    if (S.fl_tail[f] != kNone) S.it_next[S.fl_tail[f]] = (int16_t)it;
-    else S.fl_head[f] = (int16_t)it;
-    S.fl_tail[f] = (int16_t)it;
   }
 
   // A buffer's bytes as the reference leaves them: its own packet (in place)
@@ -399,6 +410,135 @@ struct Planner {
     flush_tail(c);
   }
 
+  // tcpGRO's item loop for packet bi against the items of flow f, one lane per
+  // item (lane k: the k-th item from the last, gro.go:903-951): every lane
+  // evaluates tcpPacketsCanCoalesce and coalesceTCPPackets' checks for its
+  // item from the state before this packet, without side effects, so the
+  // loop's outcome is decided at once: the first item (from the last) whose
+  // coalesce would succeed or find the packet's checksum invalid ends it; the
+  // items before it whose own checksum is invalid are deleted (deleteAt, the
+  // loop goes on past them); no such item: the packet is inserted.  Then lane 0
+  // applies the outcome.  Returns the groResult.
+  enum { W_SKIP = 0, W_DEL = 1, W_STOP = 2, W_OK = 3 };
+  __device__ int tcp_gro_wave(int bi, int f, int lane) {
+    const int base = S.fbase[f];
+    int nit = S.fnit[f];
+    int result = R_INSERT, mode = CC_UNAV, it_ok = kNone;
+    if (nit > 64) {  // wave-uniform: more items than lanes -- lane 0 runs the loop itself
+      if (lane == 0) {
+        for (int p = nit - 1; p >= 0; --p) {
+          const int it = S.fitem[base + p];
+          const int can = tcp_can(bi, it);
+          if (can == CC_UNAV) continue;
+          const int r = tcp_coalesce(can, bi, it);
+          if (r == CR_OK) {
+            result = R_COALESCED;
+            break;
+          }
+          if (r == CR_ITEM_BAD) {  // deleteAt: the items after it close up
+            S.it_alive[it] = 0;
+            for (int q = p; q + 1 < nit; ++q) S.fitem[base + q] = S.fitem[base + q + 1];
+            --nit;
+          } else if (r == CR_PKT_BAD) {
+            result = R_NOOP;
+            break;
+          }
+        }
+        if (result == R_INSERT) {
+          init_item(bi, 0);
+          S.fitem[base + nit] = (int16_t)bi;
+          ++nit;
+        }
+        S.fnit[f] = (int16_t)nit;
+        S.fl_tail[f] = nit ? S.fitem[base + nit - 1] : (int16_t)kNone;
+      }
+      return __builtin_amdgcn_readfirstlane(result);
+    }
+    {  // nit <= 64: one lane per item
+      const int k = lane;
+      int code = W_SKIP, can = CC_UNAV, it = kNone;
+      if (k < nit) {
+        it = S.fitem[base + nit - 1 - k];
+        can = tcp_can(bi, it);
+        if (can != CC_UNAV) {
+          const int s = S.it_slot[it];
+          const int pl = plen_slot(bi);
+          const int hdrs = (uint8_t)(S.it_iph[it] + S.it_l4h[it]);
+          const int new_len = plen_slot(s) + pl - hdrs;
+          const int cap = (int)S.bcap[can == CC_PREPEND ? S.sbuf[bi] : S.sbuf[s]] - offset;
+          if (cap < new_len || (can == CC_PREPEND && S.psh[bi])) code = W_SKIP;  // coalesceInsufficientCap / PSHEnding
+          else if (S.it_nm[it] == 0 && !S.valid[s]) code = W_DEL;                  // coalesceItemInvalidChecksum
+          else if (!S.valid[bi]) code = W_STOP;                                    // coalescePktInvalidChecksum
+          else code = W_OK;
+        }
+      }
+      const uint64_t dec = __ballot(code >= W_STOP);
+      const uint64_t del = __ballot(code == W_DEL) & (dec ? ((1ull << __builtin_ctzll(dec)) - 1ull) : ~0ull);
+      if (del) {  // deleteAt: the surviving items close up, in order (every lane moves its own)
+        if (k < nit && !((del >> lane) & 1ull)) {
+          const int p = nit - 1 - k;  // position from the first item
+          // deleted items below position p are those of higher lanes
+          const int np = p - (int)__builtin_popcountll(lane < 63 ? del >> (lane + 1) : 0ull);
+          S.fitem[base + np] = (int16_t)it;
+        }
+        if ((del >> lane) & 1ull) S.it_alive[it] = 0;
+      }
+      if (dec) {
+        const int d = __builtin_ctzll(dec);
+        const int cd = __shfl(code, d);
+        mode = __shfl(can, d);
+        it_ok = __shfl(it, d);
+        result = cd == W_OK ? R_COALESCED : R_NOOP;
+      }
+      nit -= (int)__builtin_popcountll(del);
+    }
+    if (lane == 0) {
+      if (result == R_COALESCED) {
+        tcp_coalesce(mode, bi, it_ok);  // its checks pass: decided above from the same state
+      } else if (result == R_INSERT) {
+        init_item(bi, 0);
+        S.fitem[base + nit] = (int16_t)bi;
+        ++nit;
+      }
+      S.fnit[f] = (int16_t)nit;
+      S.fl_tail[f] = nit ? S.fitem[base + nit - 1] : (int16_t)kNone;
+    }
+    return result;
+  }
+
+  // run_flow for a long TCP flow, by a whole wave (f wave-uniform): lane 0
+  // walks the packets and takes the in-order append fast path; a packet that
+  // leaves it goes through tcp_gro_wave (one lane per item).
+  __device__ void run_flow_wave(int f, int lane) {
+    TailCache c;
+    c.it = kNone;
+    c.dirty = false;
+    bool fresh = false;
+    for (int i = f; i != kNone;) {  // wave-uniform
+      const uint4 R = S.rec[i];
+      const int nx = (int)(int16_t)(R.z >> 16);
+      int fast = 0;
+      if (lane == 0) {
+        if (!fresh) {
+          load_tail(c, f);
+          fresh = true;
+        }
+        fast = tcp_append_fast(c, i, R) ? 1 : 0;
+        if (fast) S.res[i] = R_COALESCED;
+        else flush_tail(c);
+      }
+      if (!__builtin_amdgcn_readfirstlane(fast)) {
+        const int res = tcp_gro_wave(i, f, lane);
+        if (lane == 0) {
+          S.res[i] = (uint8_t)res;
+          fresh = false;
+        }
+      }
+      i = nx;
+    }
+    if (lane == 0) flush_tail(c);
+  }
+
   // apply{TCP,UDP}Coalesce (gro.go:1364-1366) for item `it`, or -- after
   // "invalid offset" -- nothing: its buffer keeps what the coalescing wrote
   __device__ void finish_item(int it, bool raw) {
@@ -520,7 +660,7 @@ __device__ __forceinline__ uint32_t patched(uint32_t b, int x, int iphl, int csu
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ arena, wgcs_gro_buf* __restrict__ bufs,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void gro_batch_kernel(uint8_t* __restrict__ arena, wgcs_gro_buf* __restrict__ bufs,
                                                         const wgcs_gro_call* __restrict__ calls,
                                                         int32_t* __restrict__ status, int32_t* __restrict__ n_write,
                                                         int32_t* __restrict__ to_write) {
@@ -547,6 +687,8 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
   if (t == 0) {
     S.n_eff = n;
     S.n_mat = 0;
+    S.n_coop = 0;
+    S.fitem_top = 0;
   }
   __syncthreads();
   if (t < n) {
@@ -575,6 +717,7 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
     S.res[t] = R_NOOP;
     S.it_alive[t] = 0;
     S.ndst[t] = kNone;
+    S.fsize[t] = 0;
   }
   // groCandidate + the tcpGRO / udpGRO checks that return groResultNoop
   if (t < n_eff) {
@@ -704,6 +847,7 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
       }
     }
     S.flow[t] = (uint16_t)f;
+    atomicAdd(&S.fsize[f], 1u);
     // and the next later packet of the same flow, so the flow's thread walks
     // only its own packets (each thread searches for its own link in parallel)
     int nx = kNone;
@@ -743,10 +887,20 @@ __global__ __launch_bounds__(256) void gro_batch_kernel(uint8_t* __restrict__ ar
                      (uint32_t)S.th[t] | ((uint32_t)S.iph[t] << 8) | ((uint32_t)S.psh[t] << 16) |
                          ((uint32_t)S.valid[t] << 24));
   if (live) S.rec[t] = rec;  // step 2's key-word reads ended at the barrier above
+  // a TCP flow of kCoopMin or more packets is walked by a whole wave (its
+  // item loop one lane per item, run_flow_wave); the others by one thread
+  const bool leader = live && S.flow[t] == t;
+  const bool coop = leader && S.cand[t] <= C_TCP6 && S.fsize[t] >= (uint32_t)kCoopMin;
+  if (coop) {
+    S.coop[atomicAdd(&S.n_coop, 1)] = (int16_t)t;
+    S.fbase[t] = (int16_t)atomicAdd(&S.fitem_top, (int)S.fsize[t]);  // room for one item per packet
+    S.fnit[t] = 0;
+  }
   __syncthreads();
   const bool raw = n_eff < n;  // "invalid offset": coalescing happened, apply* did not
   Planner P{S, arena, offset};
-  if (live && S.flow[t] == t) P.run_flow(t);
+  if (leader && !coop) P.run_flow(t);
+  for (int k = wv; k < S.n_coop; k += 4) P.run_flow_wave(S.coop[k], lane);  // wave-uniform
   __syncthreads();
 #ifdef WGCS_GRO_STAMPS
   stp[3] = __builtin_amdgcn_s_memrealtime();
