@@ -77,7 +77,7 @@ struct GroSmem {
   // long TCP flows walked by a whole wave (Planner::run_flow_wave): the flow's
   // packet count, its items as an array (fitem[fbase[f] .. fbase[f] + fnit[f])
   // in insertion order), the list of such flows
-  uint32_t fsize[kMaxB];
+  uint32_t fsize[kMaxB], fooo[kMaxB];  // packets of the flow, and its links out of sequence order
   int16_t fbase[kMaxB], fnit[kMaxB], fitem[kMaxB], coop[kMaxB];
   int n_eff, n_write, n_mat, n_coop, fitem_top;
 };
@@ -424,7 +424,7 @@ struct Planner {
     const int base = S.fbase[f];
     int nit = S.fnit[f];
     int result = R_INSERT, mode = CC_UNAV, it_ok = kNone;
-    if (nit > 64) {  // wave-uniform: more items than lanes -- lane 0 runs the loop itself
+    if (nit > 64 || nit <= 2) {  // wave-uniform: more items than lanes, or too few to share -- lane 0 runs the loop
       if (lane == 0) {
         for (int p = nit - 1; p >= 0; --p) {
           const int it = S.fitem[base + p];
@@ -514,9 +514,10 @@ struct Planner {
     c.it = kNone;
     c.dirty = false;
     bool fresh = false;
+    uint4 R = S.rec[f];
     for (int i = f; i != kNone;) {  // wave-uniform
-      const uint4 R = S.rec[i];
       const int nx = (int)(int16_t)(R.z >> 16);
+      const uint4 Rn = nx != kNone ? S.rec[nx] : R;  // the next record, a step ahead
       int fast = 0;
       if (lane == 0) {
         if (!fresh) {
@@ -535,6 +536,7 @@ struct Planner {
         }
       }
       i = nx;
+      R = Rn;
     }
     if (lane == 0) flush_tail(c);
   }
@@ -718,6 +720,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
     S.it_alive[t] = 0;
     S.ndst[t] = kNone;
     S.fsize[t] = 0;
+    S.fooo[t] = 0;
   }
   // groCandidate + the tcpGRO / udpGRO checks that return groResultNoop
   if (t < n_eff) {
@@ -834,7 +837,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
     const uint8_t c = S.cand[t];
     const bool v6 = c == C_TCP6 || c == C_UDP6, tcp = c <= C_TCP6;
     const int nkw = v6 ? 10 : 4;  // key words: the class fixes the layout (ack is 0 for UDP)
-    (void)tcp;
     const uint32_t kh = S.keyh[t];
     int f = t;
     for (int q = 0; q < t; ++q) {
@@ -861,6 +863,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
       }
     }
     S.fnext[t] = (int16_t)nx;
+    // a TCP packet whose successor in the flow does not continue its sequence
+    // (reordering, retransmits): appends and the fast path will not take it
+    if (tcp && nx != kNone && S.seq[nx] != S.seq[t] + S.gso[t]) atomicAdd(&S.fooo[f], 1u);
   }
   // checksumValid of every candidate: one 16-lane row per packet
   for (int p = row; p < n_eff; p += 16) {  // row-uniform
@@ -887,10 +892,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
                      (uint32_t)S.th[t] | ((uint32_t)S.iph[t] << 8) | ((uint32_t)S.psh[t] << 16) |
                          ((uint32_t)S.valid[t] << 24));
   if (live) S.rec[t] = rec;  // step 2's key-word reads ended at the barrier above
-  // a TCP flow of kCoopMin or more packets is walked by a whole wave (its
-  // item loop one lane per item, run_flow_wave); the others by one thread
+  // a TCP flow of kCoopMin or more packets, out of order in two places or
+  // more (so its packets build up several items), is walked by a whole wave
+  // (its item loop one lane per item, run_flow_wave); the others by one thread
   const bool leader = live && S.flow[t] == t;
-  const bool coop = leader && S.cand[t] <= C_TCP6 && S.fsize[t] >= (uint32_t)kCoopMin;
+  const bool coop = leader && S.cand[t] <= C_TCP6 && S.fsize[t] >= (uint32_t)kCoopMin && S.fooo[t] >= 2u;
   if (coop) {
     S.coop[atomicAdd(&S.n_coop, 1)] = (int16_t)t;
     S.fbase[t] = (int16_t)atomicAdd(&S.fitem_top, (int)S.fsize[t]);  // room for one item per packet
