@@ -77,7 +77,7 @@ struct GroSmem {
   // long TCP flows walked by a whole wave (Planner::run_flow_wave): the flow's
   // packet count, its items as an array (fitem[fbase[f] .. fbase[f] + fnit[f])
   // in insertion order), the list of such flows
-  uint32_t fsize[kMaxB], fooo[kMaxB];  // packets of the flow, and its links out of sequence order
+  uint32_t fsize[kMaxB], fooo[kMaxB];  // packets of the flow, and its links that neither append nor prepend
   int16_t fbase[kMaxB], fnit[kMaxB], fitem[kMaxB], coop[kMaxB];
   int n_eff, n_write, n_mat, n_coop, fitem_top;
 };
@@ -515,25 +515,34 @@ struct Planner {
     c.dirty = false;
     bool fresh = false;
     uint4 R = S.rec[f];
+    bool try_fast = true;
     for (int i = f; i != kNone;) {  // wave-uniform
       const int nx = (int)(int16_t)(R.z >> 16);
       const uint4 Rn = nx != kNone ? S.rec[nx] : R;  // the next record, a step ahead
       int fast = 0;
-      if (lane == 0) {
+      if (lane == 0 && try_fast) {
         if (!fresh) {
           load_tail(c, f);
           fresh = true;
         }
         fast = tcp_append_fast(c, i, R) ? 1 : 0;
-        if (fast) S.res[i] = R_COALESCED;
-        else flush_tail(c);
-      }
-      if (!__builtin_amdgcn_readfirstlane(fast)) {
-        const int res = tcp_gro_wave(i, f, lane);
-        if (lane == 0) {
-          S.res[i] = (uint8_t)res;
+        if (fast) {
+          S.res[i] = R_COALESCED;
+        } else {
+          flush_tail(c);
+          c = TailCache{};  // reloaded after the item loop: nothing of it lives across that
+          c.it = kNone;
           fresh = false;
         }
+      }
+      fast = __builtin_amdgcn_readfirstlane(fast);
+      // in a reordered flow the in-order fast path is tried again only after
+      // it last succeeded or the item loop appended to the flow's last item
+      try_fast = fast != 0;
+      if (!fast) {
+        const int res = tcp_gro_wave(i, f, lane);
+        try_fast = res == R_COALESCED && S.fl_tail[f] != kNone && S.stail[S.it_slot[S.fl_tail[f]]] == i;
+        if (lane == 0) S.res[i] = (uint8_t)res;
       }
       i = nx;
       R = Rn;
@@ -863,9 +872,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
       }
     }
     S.fnext[t] = (int16_t)nx;
-    // a TCP packet whose successor in the flow does not continue its sequence
-    // (reordering, retransmits): appends and the fast path will not take it
-    if (tcp && nx != kNone && S.seq[nx] != S.seq[t] + S.gso[t]) atomicAdd(&S.fooo[f], 1u);
+    // a TCP packet whose successor in the flow neither continues its sequence
+    // (an append) nor ends right before it (a prepend): reordering that builds
+    // up several items of the flow, which tcpGRO's item loop then scans
+    if (tcp && nx != kNone && S.seq[nx] != S.seq[t] + S.gso[t] && S.seq[nx] + S.gso[nx] != S.seq[t])
+      atomicAdd(&S.fooo[f], 1u);
   }
   // checksumValid of every candidate: one 16-lane row per packet
   for (int p = row; p < n_eff; p += 16) {  // row-uniform
@@ -892,8 +903,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
                      (uint32_t)S.th[t] | ((uint32_t)S.iph[t] << 8) | ((uint32_t)S.psh[t] << 16) |
                          ((uint32_t)S.valid[t] << 24));
   if (live) S.rec[t] = rec;  // step 2's key-word reads ended at the barrier above
-  // a TCP flow of kCoopMin or more packets, out of order in two places or
-  // more (so its packets build up several items), is walked by a whole wave
+  // a TCP flow of kCoopMin or more packets with two or more links that
+  // neither append nor prepend (so they build up several items) is walked by a whole wave
   // (its item loop one lane per item, run_flow_wave); the others by one thread
   const bool leader = live && S.flow[t] == t;
   const bool coop = leader && S.cand[t] <= C_TCP6 && S.fsize[t] >= (uint32_t)kCoopMin && S.fooo[t] >= 2u;
