@@ -36,9 +36,9 @@ if want tests; then
 fi
 if want lines; then
   line cfg2_driver 300 --gpus 1 --steps 20 --warmup 5
-  line cfg2 300 --steps 200 --warmup 20 --cpu-seconds 4
-  line cfg2_fill 300 --steps 200 --warmup 20 --mode fill --cpu-seconds 0 --no-e2e
-  line cfg2_1stream 300 --steps 200 --warmup 20 --streams 1 --cpu-seconds 0 --no-e2e
+  line cfg2 300 --steps 200 --warmup 20 --cpu-seconds 4 --no-strong
+  line cfg2_fill 300 --steps 200 --warmup 20 --mode fill --cpu-seconds 0 --no-e2e --no-strong
+  line cfg2_1stream 300 --steps 200 --warmup 20 --streams 1 --cpu-seconds 0 --no-e2e --no-strong
   line cfg3 300 --config cfg3 --steps 100 --warmup 10 --cpu-seconds 4
   line cfg5 300 --config cfg5 --steps 50 --warmup 5 --cpu-seconds 4
   line cfg4 300 --config cfg4 --steps 100 --warmup 10 --cpu-seconds 4
@@ -49,15 +49,17 @@ if want lines; then
   line gro_device 300 --config gro_device --steps 40 --warmup 4 --cpu-seconds 3
   line gro_device_1x128 300 --config gro_device --gro-shape 1x128 --steps 40 --warmup 4 --cpu-seconds 0
   line gro_device_4x32rev 300 --config gro_device --gro-shape 4x32rev --steps 20 --warmup 2 --cpu-seconds 0
+  line gro_device_shuffled 300 --config gro_device --gro-shape shuffled --steps 40 --warmup 4 --cpu-seconds 0
   line udp_split 300 --config udp_split --steps 50 --warmup 5 --cpu-seconds 3
   line udp_coalesce 300 --config udp_coalesce --steps 50 --warmup 5 --cpu-seconds 3
 fi
 if want prof; then
-  (cd /tmp && step prof_driver 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_driver" -o run --output-format csv -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --no-e2e)
+  (cd /tmp && step prof_driver 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_driver" -o run --output-format csv -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --no-e2e --no-strong)
   python3 scripts/trace_span.py "$OUT/prof_driver/run_kernel_trace.csv" checksum_batch 20 20 | sed "s/^{/{\"run\": \"prof_driver\", /" >> "$OUT/trace_span.jsonl"
-  (cd /tmp && step prof_cfg2 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg2" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e)
-  (cd /tmp && step prof_cfg2_1s 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg2_1s" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e --streams 1)
+  (cd /tmp && step prof_cfg2 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg2" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e --no-strong)
+  (cd /tmp && step prof_cfg2_1s 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg2_1s" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --cpu-seconds 0 --no-e2e --streams 1 --no-strong)
   (cd /tmp && step prof_cfg4 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg4" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 100 --warmup 10 --cpu-seconds 0 --no-e2e)
+  (cd /tmp && step prof_gro_shuffled 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_gro_shuffled" -o run --output-format csv -- python3 "$ROOT/bench.py" --config gro_device --gro-shape shuffled --steps 20 --warmup 2 --cpu-seconds 0 --no-e2e --streams 1)
   (cd /tmp && step prof_cfg4_1s 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_cfg4_1s" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 100 --warmup 10 --cpu-seconds 0 --no-e2e --streams 1)
   for d in prof_cfg2 prof_cfg2_1s prof_cfg4 prof_cfg4_1s; do
     k=checksum_batch; case $d in prof_cfg4*) k=gso_rows;; esac
@@ -65,9 +67,11 @@ if want prof; then
   done
 fi
 if want pmc; then
-  (cd /tmp && step pmcf_cfg2 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_cfg2" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 30 --warmup 3 --cpu-seconds 0 --no-e2e --no-event-timing --streams 1)
-  (cd /tmp && step pmcw_cfg2 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_cfg2" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 30 --warmup 3 --cpu-seconds 0 --no-e2e --no-event-timing --streams 1)
+  (cd /tmp && step pmcf_cfg2 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_cfg2" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 30 --warmup 3 --cpu-seconds 0 --no-e2e --no-event-timing --streams 1 --no-strong)
+  (cd /tmp && step pmcw_cfg2 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_cfg2" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 30 --warmup 3 --cpu-seconds 0 --no-e2e --no-event-timing --streams 1 --no-strong)
   (cd /tmp && step pmcf_cfg4 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_cfg4" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 30 --warmup 3 --cpu-seconds 0 --no-e2e --no-event-timing --streams 1)
   (cd /tmp && step pmcw_cfg4 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_cfg4" -o run --output-format csv -- python3 "$ROOT/bench.py" --config cfg4 --steps 30 --warmup 3 --cpu-seconds 0 --no-e2e --no-event-timing --streams 1)
+  (cd /tmp && step pmcf_gro_shuffled 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_gro_shuffled" -o run --output-format csv -- python3 "$ROOT/bench.py" --config gro_device --gro-shape shuffled --steps 10 --warmup 2 --cpu-seconds 0 --no-e2e --streams 1)
+  (cd /tmp && step pmcw_gro_shuffled 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_gro_shuffled" -o run --output-format csv -- python3 "$ROOT/bench.py" --config gro_device --gro-shape shuffled --steps 10 --warmup 2 --cpu-seconds 0 --no-e2e --streams 1)
 fi
 echo "== done"
