@@ -179,3 +179,23 @@ def test_bench_gpus_n_runs_n_ranks(n):
     assert lines[0]["n_gpus"] == n and lines[0]["value"] > 0
     assert lines[0]["config"]["parallelism"] == f"shard{n} (no collective)"
     assert bench.line_problems(lines[0]) == []
+
+
+@pytest.mark.gpu
+def test_bench_default_line_complete():
+    """The driver's invocation shape at N = 1 (cfg2, doorbell-gated steps, the
+    configs[4] strong block, the CPU baseline): one JSON line that
+    bench.line_problems accepts, with the kernel no slower than the wall clock
+    allows."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "5",
+                        "--warmup", "2", "--cpu-seconds", "0.5", "--no-e2e"], cwd=ROOT,
+                       env=_env(), capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert bench.line_problems(line) == []
+    assert "doorbell" in line["timing"]["enqueue"]
+    assert line["roofline"]["kernel_ms"] <= line["ms_per_step"] * 1.05
+    st = line["cfg5_strong"]
+    assert st["packets_per_rank"] == [1048576] and st["roofline"]["frac"] > 0
