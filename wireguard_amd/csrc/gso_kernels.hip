@@ -982,6 +982,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
     return !split_type || (plen_s > hmin && hmin + (int64_t)y * ROWS * gso_s < plen_s);
   };
   if (!group_live((int)blockIdx.y)) return;
+#ifdef WGCS_GSO_HEAD_MIN  // timing-only build: descriptor + virtio header + verdict inputs, nothing else
+  if (threadIdx.x == 0 && blockIdx.y == 0) count[jb] = ok_s ? 45 : 0;
+  if (threadIdx.x == 0 && blockIdx.y == 0) status[jb] = clean_s ? 0 : 1;
+  return;
+#endif
 
   uint4 Q;  // readBuf[16r, 16r + 16) (bytes below hdrLen)
   {
@@ -1007,6 +1012,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
       count[jb] = many ? (int)max_segs - 1 : nfull_s;
       status[jb] = many ? WGCS_ERR_TOO_MANY_SEGMENTS : 0;
     }
+#ifdef WGCS_GSO_HEAD_VERDICT  // timing-only build: the head up to the verdict (no job sums, no stream)
+    return;
+#endif
     const int type = type_s, ipv = ipv_s, hdr_len = hdr_s, gso = gso_s, cs = cs_s, co = co_s, plen = plen_s;
     // job-constant header sums from this row's own header chunks (header_fast's
     // values): IPv4 header without total length / id / checksum, the L4
