@@ -152,3 +152,38 @@ def test_stager_reserve_commit_and_errors(dev):
     st.close()
     with pytest.raises(WgcsError):  # a one-slot ring could never hand back results
         Stager(dev, depth=1, max_reads=3, max_bytes=1 << 16, max_segs=nbufs, seg_room=bufsize - OFFSET)
+
+
+def test_stager_fuzz_geometries(dev):
+    """The handleVirtioRead header-fuzz corpus (tests/gso_cases.py: IP headers
+    shorter than 6 / 20 bytes, checksum fields past hdrLen or past a short
+    segment's end, wrapped u16 positions, errors) through the read stager:
+    every read's bufs equal the oracle's byte for byte, including gsoSplit's
+    header writes past a segment's end (copy_out runs such reads again through
+    the per-call path with the caller's buffers staged)."""
+    import itertools
+
+    import gso_cases
+
+    nbufs, bufsize = 16, 9000
+    st = Stager(dev, depth=2, max_reads=32, max_bytes=32 * 65552, max_segs=nbufs, seg_room=bufsize - OFFSET)
+    cases = [c[0] for c in itertools.islice(gso_cases.fuzz_cases(False), 400)]
+    k = batches = 0
+    while k < len(cases):
+        chunk = []
+        while k < len(cases) and len(chunk) < 32:
+            try:
+                st.push(cases[k])
+            except WgcsError as e:
+                if e.code != ERR_BATCH_FULL or not chunk:
+                    raise
+                break
+            chunk.append(cases[k])
+            k += 1
+        b = st.submit()
+        st.wait(b)
+        batches += 1
+        for i, vp in enumerate(chunk):
+            _check_read(st, b, i, vp, nbufs, bufsize)
+    st.close()
+    assert batches >= 13

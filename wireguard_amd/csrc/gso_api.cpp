@@ -53,16 +53,16 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   uint32_t pitch, nseg_bound;
   gso_out_layout(vbuf, vlen, jflags, (uint32_t)kbufs, &pitch, &nseg_bound);
   if (pitch == 0) pitch = 16;
-  const size_t region = (size_t)pitch * nseg_bound;
-  // header geometry as the kernel will see it (for the per-buffer slice checks)
   const bool raw = (jflags & WGCS_GSO_JOB_RAW) != 0;
-  uint8_t gtype = vlen >= 10 ? vbuf[1] : 0;
-  uint16_t cs = 0;
-  if (vlen >= 10) memcpy(&cs, vbuf + 6, 2);
-  const bool v4 = raw ? (jflags & WGCS_GSO_JOB_V6) == 0 : (vlen > 10 && (vbuf[10] >> 4) == 4);
-  // An IPv4 header shorter than 6 bytes makes the id update read bufs[i]'s own
-  // bytes 4-5 (gro.go:1427): the kernel reads them from the segment's slot.
-  const bool stale_id = (raw || gtype != 0) && v4 && cs <= 5 && region && !nobuf;
+  const uint8_t gtype = vlen >= 10 ? vbuf[1] : 0;
+  // A header geometry whose result involves the caller's bytes beyond the
+  // packets (a field past a segment's end, or the IPv4 id update reading
+  // bufs[i][4:6], gro.go:1426-1431): the region mirrors each buffer's window
+  // -- staged in, written by the kernel with its past-the-end header writes
+  // (kOutPosTails), copied back over each segment's whole reach.
+  const bool mirror = !nobuf && gso_touches_caller_bytes(vbuf, vlen, jflags);
+  if (mirror) pitch = std::max<uint32_t>(pitch, (uint32_t)((gso_field_reach(vbuf, vlen, jflags) + 15) & ~(size_t)15));
+  const size_t region = (size_t)pitch * nseg_bound;
   hipSetDevice(ctx->device);
   int rc;
   const size_t meta = ((size_t)kbufs * 4 + 16 + 15) & ~(size_t)15;  // sizes[kbufs] | count | status
@@ -78,13 +78,14 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   hjob->flags = jflags;
   hpos->base = 0;
   hpos->pitch = pitch;
-  hpos->pad = 0;
+  hpos->flags = mirror ? kOutPosTails : 0u;
   int32_t* h = (int32_t*)hm;
   uint8_t* hs = (uint8_t*)ctx->h_stage.ptr;
-  if (stale_id) {
+  if (mirror && region) {
     memset(hs, 0, region);
     for (uint32_t i = 0; i < nseg_bound && i < (uint32_t)nbufs; ++i)
-      if (buf_lens[i] > (size_t)offset) memcpy(hs + (size_t)i * pitch, bufs[i] + offset, std::min<size_t>(6, buf_lens[i] - offset));
+      if (buf_lens[i] > (size_t)offset)
+        memcpy(hs + (size_t)i * pitch, bufs[i] + offset, std::min<size_t>(pitch, buf_lens[i] - offset));
   }
   // pinned staging is mapped into the device's address space at its host
   // address (checked by ensure_pinned's hipHostMalloc contract, see api.cpp)
@@ -121,12 +122,32 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
       res->count = i;
       return WGCS_OK;
     }
-    memcpy(bufs[i] + offset, hs + (size_t)i * pitch, (size_t)h[i]);
+    memcpy(bufs[i] + offset, hs + (size_t)i * pitch, mirror ? need : (size_t)h[i]);
   }
   return WGCS_OK;
 }
 
 }  // namespace
+
+namespace wgcs {
+
+// The per-call path for one job whose bytes the caller owns (the read stager's
+// copy_out for a geometry that touches the caller's buffers).  Takes ctx->mu.
+int gso_split_staged(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflags, uint8_t* const* bufs,
+                     const size_t* buf_lens, int nbufs, int* sizes, int offset, int* status, int* count) {
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc;
+  if ((rc = ensure_pinned(ctx, ctx->h_out, vlen + 16))) return rc;
+  if (vlen) memcpy(ctx->h_out.ptr, vbuf, vlen);
+  GsoResult r;
+  if ((rc = run_gso_host(ctx, (const uint8_t*)ctx->h_out.ptr, vlen, jflags, bufs, buf_lens, nbufs, sizes, offset, &r)))
+    return rc;
+  *status = r.status;
+  *count = r.count;
+  return WGCS_OK;
+}
+
+}  // namespace wgcs
 
 extern "C" {
 

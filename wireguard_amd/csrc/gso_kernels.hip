@@ -129,7 +129,11 @@ __device__ bool split_bounds(Job& j) {
     if (j.cs > j.hdr_len) return false;                        // pkt[csumStart:hdrLen]
     if (plen < (v4 ? 20 : 40)) return false;                   // address slices
   }
-  j.gen = !(j.cs >= (v4 ? 20 : 40) && ca + 2 <= j.hdr_len && j.hdr_len <= kMaxHdrLen);
+  // (and every per-segment L4 field inside the header: a seq / UDP length /
+  // flags byte past hdrLen can land past a short segment's end, which only the
+  // general path writes)
+  j.gen = !(j.cs >= (v4 ? 20 : 40) && ca + 2 <= j.hdr_len && j.hdr_len <= kMaxHdrLen &&
+            j.cs + (tcp ? 14 : 6) <= j.hdr_len);
   return true;
 }
 
@@ -251,7 +255,7 @@ __device__ __forceinline__ uint32_t pre_csum(const GenSeg& g, int x) {
 
 // One segment on one 16-lane row (lane r): the three passes, then sizes[].
 __device__ void gso_general_row(const uint8_t* rb, int plen, int type, int ipv, int hdr_len, int gso, int cs, int co,
-                                int i, uint8_t* dst, int r, int32_t* size_out) {
+                                int i, uint8_t* dst, int r, int32_t* size_out, bool tails) {
   GenSeg g;
   g.rb = rb;
   g.plen = plen;
@@ -319,6 +323,41 @@ __device__ void gso_general_row(const uint8_t* rb, int plen, int type, int ipv, 
       w[b >> 2] |= v << (8 * (b & 3));
     }
     store_chunk(dbase + 16 * k, make_uint4(w[0], w[1], w[2], w[3]), x0, g.pkt_len);
+  }
+  // The header writes that land past the packet's end (a header geometry with
+  // fields beyond hdrLen and a short segment): gsoSplit writes them into
+  // bufs[i] all the same, in its order -- id / length / IPv4 checksum (:1426-
+  // 1439), seq + flags or UDP length (:1443-1466), the L4 checksum last
+  // (:1485-1488).  Every position lies inside the slot: the decoder refused
+  // (OUT_OF_RANGE) a slot shorter than segment 0's reach (split_need).  A
+  // packed host region sized for the packets alone says !tails (GsoOutPos).
+  if (r == 0 && tails) {
+    auto put = [&](int x, uint32_t v) {
+      if (x >= g.pkt_len) dst[x] = (uint8_t)v;
+    };
+    if (g.v4) {
+      if (i > 0) {
+        put(4, g.id45 >> 8);
+        put(5, g.id45 & 0xFFu);
+      }
+      put(2, ((uint32_t)g.pkt_len >> 8) & 0xFFu);
+      put(3, (uint32_t)g.pkt_len & 0xFFu);
+      put(10, g.ipc >> 8);
+      put(11, g.ipc & 0xFFu);
+    } else {
+      const uint32_t pl = (uint32_t)(g.pkt_len - cs) & 0xFFFFu;
+      put(4, pl >> 8);
+      put(5, pl & 0xFFu);
+    }
+    if (g.tcp) {
+      for (int t = 0; t < 4; ++t) put(g.s4 + t, (g.seq >> (24 - 8 * t)) & 0xFFu);
+      if (!g.last && g.f13 >= g.pkt_len) dst[g.f13] = (uint8_t)(dst[g.f13] & ~0x09u);
+    } else {
+      put(g.s4, g.ulen >> 8);
+      put(g.s4 + 1, g.ulen & 0xFFu);
+    }
+    put(g.ca, l4c >> 8);
+    put(g.ca + 1, l4c & 0xFFu);
   }
   if (r == 0) *size_out = g.pkt_len;
 }
@@ -800,7 +839,8 @@ __device__ __forceinline__ void finish_row(bool fast, const uint4 Q, int type, i
 template <int U, bool NT>
 __device__ __noinline__ int decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, uint32_t jflags_a, uint32_t room,
                                           uint32_t max_segs, int i, bool first_block, int32_t* count_j,
-                                          int32_t* status_j, uint8_t* out0, uint8_t* dst, int32_t* sizes_j) {
+                                          int32_t* status_j, uint8_t* out0, uint8_t* dst, int32_t* sizes_j,
+                                          uint32_t tails_a) {
   __shared__ JobInfo ji;
   const uint4 z = make_uint4(0, 0, 0, 0);
   const int lane = threadIdx.x & 63;
@@ -845,7 +885,7 @@ __device__ __noinline__ int decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, u
   const int cs = ufl(ji.cs);
   const int co = ufl(ji.co);
   if ((shape >> 16) & 0xFFu) {  // block-uniform
-    gso_general_row(rb, plen, type, ipv, hdr_len, gso, cs, co, i, dst, r, sizes_j + i);
+    gso_general_row(rb, plen, type, ipv, hdr_len, gso, cs, co, i, dst, r, sizes_j + i, ufl((int)tails_a) != 0);
     return nseg;
   }
   uint32_t acc = 0;
@@ -907,9 +947,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   // or the caller's packed per-job layout (the stager's compact D2H region)
   uint64_t obase = slot0 * out_stride;
   uint32_t opitch = out_stride;
+  uint32_t tails = 1;  // gsoSplit's header writes past a segment's end (GsoOutPos)
   if (outpos) {
     obase = outpos[jb].base;
     opitch = outpos[jb].pitch;
+    tails = outpos[jb].flags & kOutPosTails;
   }
   // ---- header chunks in packet coordinates (lane r of each row: the
   // dword-aligned 16-byte window r from the dword holding readBuf[0]; shifted
@@ -1085,7 +1127,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
       const int i = grp * ROWS + wv * 4 + (lane >> 4);
       uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
       const int live = decoded_rows<U, NT>(vb, jlen, job.flags, room, max_segs, i, grp == 0, &count[jb], &status[jb],
-                                           out + obase + offset, dst, &sizes[slot0]);
+                                           out + obase + offset, dst, &sizes[slot0], tails);
       lds_barrier();  // every wave is done with this group's verdict before the next one is published
       // the verdict bounds the job's segments (0 for an error / GSO_NONE): no
       // decode + barrier round for groups past it, whatever max_segs is

@@ -144,7 +144,7 @@ int finish(wgcs_stager* st, size_t n) {
   s.h_jobs[r].flags = 0;
   s.h_pos[r].base = s.used_out;
   s.h_pos[r].pitch = pitch ? pitch : 16;
-  s.h_pos[r].pad = 0;
+  s.h_pos[r].flags = 0;  // packets only: copy_out applies the rest
   s.used_in += align16(n);
   s.used_out += region;
   s.n_reads++;
@@ -375,6 +375,17 @@ int wgcs_stager_copy_out(wgcs_stager* st, uint64_t batch, int read_idx, uint8_t*
   const uint32_t pitch = s->h_pos[read_idx].pitch;
   const uint8_t* vb = s->h_in + s->h_jobs[read_idx].off;
   const size_t vlen = s->h_jobs[read_idx].len;
+  if (gso_touches_caller_bytes(vb, vlen, 0)) {
+    // A header geometry whose result involves the caller's buffers beyond the
+    // packets (a field past a segment's end, or the IPv4 id update reading
+    // bufs[i][4:6]): the batch kernel wrote the packets only; the read runs
+    // again on the GPU through the per-call path, with these buffers staged.
+    int st2 = 0, n2 = 0;
+    const int rc = gso_split_staged(st->ctx, vb, vlen, 0, bufs, buf_lens, nbufs, sizes, offset, &st2, &n2);
+    if (rc) return rc;
+    *n_out = n2;
+    return st2;
+  }
   const int written = status == WGCS_ERR_TOO_MANY_SEGMENTS ? nbufs : n;
   for (int i = 0; i < written; ++i) {
     sizes[i] = sz[i];

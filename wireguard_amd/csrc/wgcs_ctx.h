@@ -33,6 +33,11 @@ bool host_mapped_locked(wgcs_ctx* ctx, const void* p, size_t n);
 // A live write-stager slot (open, or submitted and not yet finished) still
 // reads [a, b) through a zero-copy push (wstager.cpp); caller holds host_mu.
 bool wstager_references(wgcs_wstager* ws, uintptr_t a, uintptr_t b);
+// handleVirtioRead / gsoSplit of one job ([virtio header | packet], vlen
+// bytes, not modified) into the caller's buffers through the per-call path
+// (gso_api.cpp); takes ctx->mu.  Lock order: a read stager's mu before ctx->mu.
+int gso_split_staged(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflags, uint8_t* const* bufs,
+                     const size_t* buf_lens, int nbufs, int* sizes, int offset, int* status, int* count);
 
 }  // namespace wgcs
 
@@ -51,7 +56,7 @@ struct wgcs_ctx {
   // wgcs_host_alloc allocations (device-readable pinned memory): [start, end),
   // the live write stagers, whose zero-copy pushes point into them, and the
   // live read stagers (wgcs_destroy refuses while any stager is alive).  Lock
-  // order: host_mu before a write stager's mu.
+  // order: host_mu before a write stager's mu; a read stager's mu before mu.
   std::mutex host_mu;
   std::vector<std::pair<uintptr_t, uintptr_t>> host_allocs;
   std::vector<wgcs_wstager*> wstagers;

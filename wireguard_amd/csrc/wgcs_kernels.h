@@ -24,11 +24,16 @@ hipError_t launch_checksum_batch(int mode, unsigned flags, uint8_t* arena, const
 // Optional packed output layout: segment i of job j at out + base + i*pitch
 // (+ offset); pitch must hold the job's largest segment.  The room checks
 // (handleVirtioRead's bufs element length) then use `room` instead of
-// out_stride - offset.
+// out_stride - offset.  Without kOutPosTails the kernel writes the packets
+// only: gsoSplit's header writes that land past a segment's end (a field
+// beyond hdrLen) are skipped, so a pitch sized for the packets is never
+// overrun.  With it (the caller's buffers staged into the region, a pitch of
+// at least gso_field_reach) they are written as into fixed slots.
+enum : uint32_t { kOutPosTails = 1 };
 struct GsoOutPos {
   uint64_t base;
   uint32_t pitch;
-  uint32_t pad;
+  uint32_t flags;  // kOutPosTails
 };
 // Packed-layout pitch and segment bound of one job ([10-byte virtio header |
 // packet], n bytes) from its virtio header and job flags: every segment
@@ -79,6 +84,35 @@ inline size_t gso_split_need(const uint8_t* vb, size_t n, uint32_t jflags, size_
   if (tcp && !last && (f = (size_t)(uint16_t)(cs + 13) + 1) > need) need = f;
   if ((f = (size_t)(uint16_t)(cs + co) + 2) > need) need = f;
   return need;
+}
+
+// gsoSplit's fixed-position header writes' reach for job vb: the last byte + 1
+// of IPv4 [2:12) / IPv6 [4:6), seq or UDP length, the flags byte (non-last
+// segments) and the checksum field.
+inline size_t gso_field_reach(const uint8_t* vb, size_t n, uint32_t jflags) {
+  return gso_split_need(vb, n, jflags, 0, false);
+}
+
+// Does gsoSplit's result for job vb involve bytes of bufs[i] other than the
+// segments it produces?  Either a header write can land past a segment's end
+// (a field beyond the smallest hdrLen the job can have), or the IPv4 id update
+// reads bufs[i][4:6] (an IP header shorter than 6 bytes, gro.go:1426-1431).
+// Host entry points then stage the caller's buffers through the kernel.
+// Never for a well-formed TCP / UDP header (every field inside hdrLen).
+inline bool gso_touches_caller_bytes(const uint8_t* vb, size_t n, uint32_t jflags) {
+  if (n <= 10) return false;
+  const bool raw = (jflags & WGCS_GSO_JOB_RAW) != 0;
+  const uint8_t t = vb[1];
+  if (!raw && t == 0) return false;  // GSO_NONE: the packet only
+  const bool v4 = raw ? (jflags & WGCS_GSO_JOB_V6) == 0 : (vb[10] >> 4) == 4;
+  const bool tcp = t == 1 || t == 4;
+  const size_t cs = (size_t)vb[6] | ((size_t)vb[7] << 8);
+  if (v4 && cs <= 5) return true;
+  size_t lb;  // hdrLen's lower bound (handleVirtioRead's u16 recompute may wrap: then 0)
+  if (raw) lb = (size_t)vb[2] | ((size_t)vb[3] << 8);
+  else if (tcp) lb = cs + 60 <= 0xFFFF ? cs + 20 : 0;
+  else lb = cs + 8 <= 0xFFFF ? cs + 8 : 0;
+  return gso_field_reach(vb, n, jflags) > lb;
 }
 
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs,

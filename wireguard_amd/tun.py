@@ -44,7 +44,8 @@ def set_pkt_off(pkts: np.ndarray, off) -> None:
 def pkt_off(pkts: np.ndarray) -> np.ndarray:
     """Arena offsets of a PKT_DTYPE array (uint64)."""
     return pkts["off_lo"].astype(np.uint64) | (pkts["off_hi"].astype(np.uint64) << np.uint64(32))
-GSO_JOB_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("pad", "<u4")])
+GSO_JOB_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("flags", "<u4")])  # wgcs_gso_job
+GSO_JOB_RAW, GSO_JOB_V6 = 0x1, 0x2  # WGCS_GSO_JOB_*: gsoSplit with the job's own virtio header / isV6
 # wgcs_batch (include/wgcsum.h): one batch of wgcs_checksum_batches
 BATCH_DTYPE = np.dtype([("arena", "<u8"), ("pkts", "<u8"), ("initial", "<u8"), ("out", "<u8"), ("n", "<u4"),
                         ("pad", "<u4")])
