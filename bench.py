@@ -73,6 +73,10 @@ def parse():
                     help="gro_device: the packets of each Write call (wireguard_amd/gro_bench.py CALL_SHAPES)")
     ap.add_argument("--max-segs", type=int, default=128,
                     help="cfg4: output slots per read = len(bufs) (the reference's Read passes conn.BatchSize = 128)")
+    ap.add_argument("--gso-out-align", type=int, default=128,
+                    help="cfg4: output slots placed so that bufs[i][offset] starts on this many bytes (0: as allocated)")
+    ap.add_argument("--gso-in-align", type=int, default=128,
+                    help="cfg4: each read's buffer at a multiple of this many bytes in the arena (0: packed)")
     ap.add_argument("--verify", action="store_true", help="check the GPU results against the synth ground truth")
     ap.add_argument("--no-strong", action="store_true",
                     help="cfg2: skip the configs[4] block (the 1M mixed batch split over the ranks, `cfg5_strong`)")

@@ -27,16 +27,24 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
     R = max(args.rotate, 8)  # (16.8 MB in + 25 MB out) per copy: rotate past the 256 MiB MALL
     pkts = [synth.make_super_packet(total, gso, seed=synth.SEED + 1000 * rank + k) for k in range(n_jobs)]
     jlen = len(pkts[0])
-    arena = np.frombuffer(b"".join(pkts) + bytes(64), dtype=np.uint8).copy()  # 64 B of slack past the last job
+    in_align = getattr(args, "gso_in_align", 0) or 1
+    jpitch = -(-jlen // in_align) * in_align
+    arena = np.zeros(n_jobs * jpitch + 64, np.uint8)  # 64 B of slack past the last job
+    for k, p in enumerate(pkts):
+        arena[k * jpitch: k * jpitch + jlen] = np.frombuffer(p, np.uint8)
     jobs = np.zeros(n_jobs, GSO_JOB_DTYPE)
-    jobs["off"] = np.arange(n_jobs, dtype=np.uint64) * np.uint64(jlen)
+    jobs["off"] = np.arange(n_jobs, dtype=np.uint64) * np.uint64(jpitch)
     jobs["len"] = jlen
+    out_align = getattr(args, "gso_out_align", 0)
+    # slot base shift so that bufs[i][offset] lands on an out_align boundary (stride is a multiple of 128)
+    oshift = (out_align - offset % out_align) % out_align if out_align else 0
     S = max(1, getattr(args, "streams", 1))
     streams = [torch.cuda.Stream() for _ in range(S)]
     R = max(R, 2 * S)
     d_arena = [torch.from_numpy(arena).cuda() for _ in range(R)]
     d_jobs = torch.from_numpy(jobs.view(np.uint8)).cuda()
-    d_out = [torch.empty(n_jobs * max_segs * stride, dtype=torch.uint8, device="cuda") for _ in range(R)]
+    d_out = [torch.empty(n_jobs * max_segs * stride + 256, dtype=torch.uint8, device="cuda")[oshift:]
+             for _ in range(R)]
     # per-stream result arrays: launches on different streams may overlap
     d_sizes = [torch.zeros(n_jobs * max_segs, dtype=torch.int32, device="cuda") for _ in range(S)]
     d_count = [torch.zeros(n_jobs, dtype=torch.int32, device="cuda") for _ in range(S)]
@@ -124,6 +132,8 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
             "bytes_in": bytes_in,
             "bytes_out": bytes_out,
             "rotated_copies": R,
+            "out_align": out_align,
+            "in_align": in_align,
             "streams": S,
             "parallelism": f"shard{world} (no collective)",
         },
