@@ -73,6 +73,8 @@ def parse():
                     help="gro_device: the packets of each Write call (wireguard_amd/gro_bench.py CALL_SHAPES)")
     ap.add_argument("--max-segs", type=int, default=128,
                     help="cfg4: output slots per read = len(bufs) (the reference's Read passes conn.BatchSize = 128)")
+    ap.add_argument("--frame-stride", type=int, default=0,
+                    help="cfg1-3: frame k at k * stride in the arena (0: back to back, the frame length)")
     ap.add_argument("--gso-out-align", type=int, default=128,
                     help="cfg4: output slots placed so that bufs[i][offset] starts on this many bytes (0: as allocated)")
     ap.add_argument("--gso-in-align", type=int, default=128,
@@ -197,7 +199,8 @@ def main():
     if scaling == "strong":
         arena_np, pkts_np, _, lo, hi = shard.make_global_shard(n_cfg, rank, world, flen, kinds)
     else:  # every rank its own seeded 64k batch
-        arena_np, pkts_np, _ = synth.make_batch(n_cfg, flen, kinds=kinds, seed=synth.SEED + rank)
+        arena_np, pkts_np, _ = synth.make_batch(n_cfg, flen, kinds=kinds, seed=synth.SEED + rank,
+                                                stride=args.frame_stride or None)
     n = len(pkts_np)
     bytes_per_step = int(pkts_np["len"].astype(np.int64).sum())
     use_events = not args.no_event_timing
@@ -237,6 +240,7 @@ def main():
             "global_batch_bytes": bytes_per_step * world if scaling == "weak" else n_cfg * flen,
             "mode": args.mode,
             "rotated_copies": R,
+            "frame_stride": args.frame_stride or flen,
             "streams": S,
             "parallelism": f"shard{world} (no collective)",
         },

@@ -23,6 +23,7 @@
  *   wgcs_gso_split            gsoSplit(readBuf, hdr, bufs, sizes, offset, isV6)  tun/gro.go:1373-1493
  *   wgcs_gso_split_batch      device-resident batch of gsoSplit calls  (one per Tun.Read)
  *   wgcs_handle_virtio_read   handleVirtioRead(readBuf, bufs, sizes, offset)  tun/tun.go:514-632
+ *   wgcs_*_cap                the same two with cap(readBuf)  (spare capacity, gro.go:1471-1477)
  *   wgcs_handle_gro           handleGRO(bufs, offset, tcpTable, udpTable, canUDPGRO, &toWrite)
  *                                                                 tun/gro.go:1326-1367
  *   wgcs_handle_gro_batch     device-resident batch of handleGRO calls (one per Tun.Write)
@@ -134,6 +135,12 @@ typedef struct wgcs_gso_job {
  * given (gro.go:1373-1493); WGCS_GSO_JOB_V6 then gives isV6. */
 #define WGCS_GSO_JOB_RAW 0x1u
 #define WGCS_GSO_JOB_V6 0x2u
+/* bits 8-15: how many bytes after the job's len bytes in the arena belong to
+ * the read buffer's spare capacity (cap(readBuf) - len(readBuf), at most 255).
+ * The pseudo-header address slices of a packet shorter than 20 / 40 bytes
+ * reach into it (gro.go:1471-1477: a slice up to cap is legal Go); past it
+ * the reference panics (OUT_OF_RANGE).  0: cap == len. */
+#define WGCS_GSO_JOB_SPARE(n) ((uint32_t)((n) > 255 ? 255 : (n)) << 8)
 
 /* ---- lifecycle / diagnostics ---- */
 int wgcs_abi_version(void);
@@ -161,7 +168,12 @@ int wgcs_host_free(wgcs_ctx *ctx, void *p);
 
 /* ---- device-resident batch entry points (HBM in, HBM out; async on stream) ----
  * The arena must be readable through align_up(off+len, 16) for every packet
- * (always true for hipMalloc / torch allocations, which are page-granular). */
+ * (always true for hipMalloc / torch allocations, which are page-granular).
+ * VALIDATE / L4_FILL read the pseudo-header addresses at [12, 20) / [8, 40)
+ * whatever len is: a packet shorter than them has them read from the arena
+ * bytes after it, its Go slice's spare capacity (gro.go:558-563), which must
+ * then be readable too.  A csum_start past len (pkt[iphLen:] panics in Go)
+ * gives VALIDATE 0 and L4_FILL 0 with no field write. */
 int wgcs_checksum_batch(wgcs_ctx *ctx, int mode, unsigned flags, uint8_t *d_arena,
                         const wgcs_pkt *d_pkts, const uint64_t *d_initial, uint32_t n,
                         void *d_out, void *stream);
@@ -216,6 +228,12 @@ int wgcs_gso_split_batch(wgcs_ctx *ctx, const uint8_t *d_arena, const wgcs_gso_j
 int wgcs_checksum(wgcs_ctx *ctx, const uint8_t *b, size_t n, uint64_t initial, uint16_t *out);
 int wgcs_checksum_valid(wgcs_ctx *ctx, const uint8_t *pkt, size_t len, uint8_t iph_len,
                         uint8_t proto, int is_v6, int *valid);
+/* the same with the slice's capacity: pkt[0, cap) is readable, and a packet
+ * shorter than its addresses (20 / 40 B) has them read from pkt[len, cap), as
+ * Go's pkt[a:b] up to cap does (gro.go:558-563); OUT_OF_RANGE past cap or for
+ * iph_len > len.  wgcs_checksum_valid is this with cap == len. */
+int wgcs_checksum_valid_cap(wgcs_ctx *ctx, const uint8_t *pkt, size_t len, size_t cap,
+                            uint8_t iph_len, uint8_t proto, int is_v6, int *valid);
 int wgcs_gso_none_checksum(wgcs_ctx *ctx, uint8_t *read_buf, size_t len, uint16_t csum_start,
                            uint16_t csum_offset);
 /* host batch: same semantics as wgcs_checksum_batch on a host arena */
@@ -230,6 +248,17 @@ int wgcs_gso_split(wgcs_ctx *ctx, uint8_t *read_buf, size_t len, const wgcs_virt
 int wgcs_handle_virtio_read(wgcs_ctx *ctx, uint8_t *read_buf, size_t n, uint8_t *const *bufs,
                             const size_t *buf_lens, int nbufs, int *sizes, int offset,
                             int *n_out);
+/* The same with the slice's capacity: read_buf[0, cap) is readable and
+ * read_buf[n, cap) is the spare capacity Tun.Read's tun.readBuf[:n] carries
+ * (tun/tun.go:484-503); only the pseudo-header address slices of a packet
+ * shorter than its IP addresses reach it (gro.go:1471-1477).  cap >= n;
+ * wgcs_handle_virtio_read is this with cap == n.  Same for gsoSplit. */
+int wgcs_handle_virtio_read_cap(wgcs_ctx *ctx, uint8_t *read_buf, size_t n, size_t cap,
+                                uint8_t *const *bufs, const size_t *buf_lens, int nbufs,
+                                int *sizes, int offset, int *n_out);
+int wgcs_gso_split_cap(wgcs_ctx *ctx, uint8_t *read_buf, size_t len, size_t cap,
+                       const wgcs_virtio_hdr *hdr, uint8_t *const *bufs, const size_t *buf_lens,
+                       int nbufs, int *sizes, int offset, int is_v6, int *n_out);
 /* Go-slice form of handleGRO: lens[i] = len(bufs[i]), caps[i] = cap(bufs[i]).
  * bufs/lens/caps are updated in place (appends grow lens[i]; prepends swap
  * entries, gro.go:696-697); to_write receives the indices to write. */

@@ -58,6 +58,11 @@ def lib() -> C.CDLL:
             C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_int),
         ]
         L.or_handle_virtio_read.restype = C.c_int
+        L.or_handle_virtio_read_cap.argtypes = [
+            C.c_void_p, C.c_size_t, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.c_int,
+            C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_int),
+        ]
+        L.or_handle_virtio_read_cap.restype = C.c_int
         L.or_handle_gro.argtypes = [
             C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.c_int, C.c_int, C.c_int,
             C.POINTER(C.c_int), C.POINTER(C.c_int),
@@ -100,9 +105,18 @@ def pseudo_header_nofold(src: bytes, dst: bytes, proto: int, total_len: int) -> 
     return lib().or_pseudo_header_nofold(_ptr(s), _ptr(d), len(src), proto, total_len & 0xFFFF)
 
 
-def checksum_valid(pkt: bytes, iph_len: int, proto: int, is_v6: bool) -> bool:
+def checksum_valid(pkt: bytes, iph_len: int, proto: int, is_v6: bool, n: int | None = None):
+    """checksumValid(pkt[:n], ...) with cap len(pkt) (n: the whole of pkt).
+    True / False, or the OUT_OF_RANGE code where Go panics."""
+    L = lib()
+    if not getattr(L, "_valid_cap_ready", False):
+        L.or_checksum_valid_cap.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_uint8, C.c_uint8, C.c_int]
+        L.or_checksum_valid_cap.restype = C.c_int
+        L._valid_cap_ready = True
     a = np.frombuffer(bytes(pkt) + b"\0", dtype=np.uint8)
-    return bool(lib().or_checksum_valid(_ptr(a), len(pkt), iph_len, proto, int(is_v6)))
+    ln = len(pkt) if n is None else n
+    rc = L.or_checksum_valid_cap(_ptr(a), ln, len(pkt), iph_len, proto, int(is_v6))
+    return rc if rc < 0 else bool(rc)
 
 
 def checksum_batch(mode: int, arena: np.ndarray, pkts: np.ndarray, initial=None, inplace=False):
@@ -173,14 +187,19 @@ def _bufs_ctypes(bufs):
     return arr
 
 
-def handle_virtio_read(read_buf: bytearray, bufs: list, offset: int):
+def handle_virtio_read(read_buf: bytearray, bufs: list, offset: int, n_read: int | None = None):
     """Oracle handleVirtioRead.  Mutates read_buf (like the reference) and the
-    numpy bufs.  Returns (rc, n, sizes)."""
+    numpy bufs.  With n_read, the read is read_buf[:n_read] and the rest of
+    read_buf its spare capacity (Tun.Read's tun.readBuf[:n]).  Returns
+    (rc, n, sizes)."""
     rb = np.frombuffer(read_buf, dtype=np.uint8) if not isinstance(read_buf, np.ndarray) else read_buf
     lens = (C.c_size_t * len(bufs))(*[len(b) for b in bufs])
     sizes = (C.c_int * len(bufs))()
     n = C.c_int(0)
-    rc = lib().or_handle_virtio_read(_ptr(rb), len(rb), _bufs_ctypes(bufs), lens, len(bufs), sizes, offset, C.byref(n))
+    nr = len(rb) if n_read is None else n_read
+    assert 0 <= nr <= len(rb)
+    rc = lib().or_handle_virtio_read_cap(_ptr(rb) if len(rb) else None, nr, len(rb), _bufs_ctypes(bufs), lens,
+                                         len(bufs), sizes, offset, C.byref(n))
     return rc, n.value, list(sizes)
 
 
@@ -189,23 +208,27 @@ class VirtioHdr(C.Structure):  # or_virtio_hdr (gro.go:42-67)
                 ("csum_start", C.c_uint16), ("csum_offset", C.c_uint16)]
 
 
-def gso_split(read_buf, hdr: tuple, bufs: list, offset: int, is_v6: bool):
+def gso_split(read_buf, hdr: tuple, bufs: list, offset: int, is_v6: bool, n_read: int | None = None):
     """Oracle gsoSplit(readBuf, hdr, bufs, sizes, offset, isV6).  hdr =
     (flags, gso_type, hdr_len, gso_size, csum_start, csum_offset).  Mutates
-    read_buf and bufs.  Returns (rc, n, sizes)."""
+    read_buf and bufs.  With n_read, readBuf is read_buf[:n_read] with the
+    rest as its spare capacity.  Returns (rc, n, sizes)."""
     L = lib()
     if not getattr(L, "_split_ready", False):
         u8p = C.POINTER(C.c_uint8)
-        L.or_gso_split.argtypes = [C.c_void_p, C.c_size_t, VirtioHdr, C.POINTER(u8p), C.POINTER(C.c_size_t), C.c_int,
-                                   C.POINTER(C.c_int), C.c_int, C.c_int, C.POINTER(C.c_int)]
-        L.or_gso_split.restype = C.c_int
+        L.or_gso_split_cap.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, VirtioHdr, C.POINTER(u8p),
+                                       C.POINTER(C.c_size_t), C.c_int, C.POINTER(C.c_int), C.c_int, C.c_int,
+                                       C.POINTER(C.c_int)]
+        L.or_gso_split_cap.restype = C.c_int
         L._split_ready = True
     rb = np.frombuffer(read_buf, dtype=np.uint8) if not isinstance(read_buf, np.ndarray) else read_buf
     lens = (C.c_size_t * len(bufs))(*[len(b) for b in bufs])
     sizes = (C.c_int * len(bufs))()
     n = C.c_int(0)
-    rc = L.or_gso_split(_ptr(rb) if len(rb) else None, len(rb), VirtioHdr(*hdr), _bufs_ctypes(bufs), lens, len(bufs),
-                        sizes, offset, int(is_v6), C.byref(n))
+    nr = len(rb) if n_read is None else n_read
+    assert 0 <= nr <= len(rb)
+    rc = L.or_gso_split_cap(_ptr(rb) if len(rb) else None, nr, len(rb), VirtioHdr(*hdr), _bufs_ctypes(bufs), lens,
+                            len(bufs), sizes, offset, int(is_v6), C.byref(n))
     return rc, n.value, list(sizes)
 
 

@@ -401,22 +401,24 @@ def _np_slices(bufs):
     return [Slice(b) for b in bufs]
 
 
-def run_handle_virtio_read(read_buf: np.ndarray, bufs: list, offset: int):
+def run_handle_virtio_read(read_buf: np.ndarray, bufs: list, offset: int, n_read: int | None = None):
     """oracle.handle_virtio_read's interface: mutates read_buf and the numpy
-    bufs in place; returns (rc, n, sizes).  A Go panic is (OUT_OF_RANGE, 0, sizes)."""
+    bufs in place; returns (rc, n, sizes).  A Go panic is (OUT_OF_RANGE, 0, sizes).
+    With n_read, readBuf is read_buf[:n_read] with capacity len(read_buf)."""
     sizes = [0] * len(bufs)
     try:
-        n, rc = handle_virtio_read(Slice(read_buf), _np_slices(bufs), sizes, offset)
+        n, rc = handle_virtio_read(Slice(read_buf, 0, n_read), _np_slices(bufs), sizes, offset)
     except GoPanic:
         return ERR_OUT_OF_RANGE, 0, sizes
     return rc, n, sizes
 
 
-def run_gso_split(read_buf: np.ndarray, hdr: tuple, bufs: list, offset: int, is_v6: bool):
+def run_gso_split(read_buf: np.ndarray, hdr: tuple, bufs: list, offset: int, is_v6: bool,
+                  n_read: int | None = None):
     """oracle.gso_split's interface (hdr = the six virtio header fields)."""
     sizes = [0] * len(bufs)
     try:
-        n, rc = gso_split(Slice(read_buf), VirtioHdr(*hdr), _np_slices(bufs), sizes, offset, is_v6)
+        n, rc = gso_split(Slice(read_buf, 0, n_read), VirtioHdr(*hdr), _np_slices(bufs), sizes, offset, is_v6)
     except GoPanic:
         return ERR_OUT_OF_RANGE, 0, sizes
     return rc, n, sizes

@@ -120,12 +120,15 @@ enum { VNET_LEN = 10, F_NEEDS_CSUM = 1, GSO_NONE = 0, GSO_TCPV4 = 1, GSO_TCPV6 =
        GSO_UDP_L4 = 5 };
 enum { TCP_FLAGS_OFF = 13, TCP_FIN = 0x01, TCP_PSH = 0x08, TCP_ACK = 0x10, UDPH_LEN = 8 };
 
-/* gro.go:554-612 */
-static int checksum_valid_at(const uint8_t *pkt, size_t len, size_t iph_len,
+/* gro.go:554-612.  The address slices pkt[a:b] (:558-563) are bounded by
+ * cap(pkt), not len: a packet shorter than its addresses reads them from the
+ * bytes after it (the caller guarantees pkt[0, cap)); pkt[iphLen:] (:611) is
+ * bounded by len.  Returns 1 / 0, or OR_ERR_OUT_OF_RANGE where Go panics. */
+static int checksum_valid_at(const uint8_t *pkt, size_t len, size_t cap, size_t iph_len,
                              uint8_t proto, int is_v6) {
   size_t src_at = is_v6 ? IPV6_SRC : IPV4_SRC;
   size_t addr = is_v6 ? 16 : 4;
-  if (len < src_at + 2 * addr || len < iph_len) return 0; /* would panic */
+  if (cap < src_at + 2 * addr || len < iph_len) return OR_ERR_OUT_OF_RANGE; /* would panic */
   uint16_t total_len = (uint16_t)(len - iph_len);
   uint64_t ph = or_pseudo_header_nofold(pkt + src_at, pkt + src_at + addr, addr,
                                         proto, total_len);
@@ -133,7 +136,11 @@ static int checksum_valid_at(const uint8_t *pkt, size_t len, size_t iph_len,
 }
 int or_checksum_valid(const uint8_t *pkt, size_t len, uint8_t iph_len,
                       uint8_t proto, int is_v6) {
-  return checksum_valid_at(pkt, len, iph_len, proto, is_v6);
+  return checksum_valid_at(pkt, len, len, iph_len, proto, is_v6);
+}
+int or_checksum_valid_cap(const uint8_t *pkt, size_t len, size_t cap, uint8_t iph_len,
+                          uint8_t proto, int is_v6) {
+  return checksum_valid_at(pkt, len, cap, iph_len, proto, is_v6);
 }
 
 /* gro.go:1497-1517 */
@@ -149,11 +156,13 @@ int or_gso_none_checksum(uint8_t *rb, size_t len, uint16_t csum_start,
 
 /* gro.go:1373-1493.  Every index the reference computes from hdr fields is a
  * uint16 sum (hdr.csumStart+4, +tcpFlagsOffset, +hdr.csumOffset wrap at
- * 2^16); slices of readBuf are bounded by len(readBuf) here (see
- * or_gso_split_need for the bufs side). */
-int or_gso_split(uint8_t *rb, size_t len, or_virtio_hdr hdr,
-                 uint8_t *const *bufs, const size_t *buf_lens, int nbufs,
-                 int *sizes, int offset, int is_v6, int *n_out) {
+ * 2^16); indexes of readBuf are bounded by len(readBuf), and its slices by
+ * cap(readBuf): rb[len, cap) is the read buffer's spare capacity, which the
+ * pseudo-header address slices reach for a packet shorter than 20 / 40 bytes
+ * (:1471-1477; see or_gso_split_need for the bufs side). */
+int or_gso_split_cap(uint8_t *rb, size_t len, size_t cap, or_virtio_hdr hdr,
+                     uint8_t *const *bufs, const size_t *buf_lens, int nbufs,
+                     int *sizes, int offset, int is_v6, int *n_out) {
   int iph_len = hdr.csum_start;
   int src_off = IPV6_SRC, addr_len = 16;
   *n_out = 0;
@@ -179,10 +188,9 @@ int or_gso_split(uint8_t *rb, size_t len, or_virtio_hdr hdr,
   size_t next = hdr.hdr_len;
   if (next < len) {
     /* the loop runs: pkt[csumStart:hdrLen] panics if csumStart > hdrLen; the
-     * pseudo-header address slices reach past len(readBuf) below 20 / 40
-     * bytes (Go would read readBuf's spare capacity: not a defined input) */
+     * pseudo-header address slices panic past cap(readBuf) */
     if (hdr.csum_start > hdr.hdr_len) return OR_ERR_OUT_OF_RANGE;
-    if ((size_t)(src_off + 2 * addr_len) > len) return OR_ERR_OUT_OF_RANGE;
+    if ((size_t)(src_off + 2 * addr_len) > cap) return OR_ERR_OUT_OF_RANGE;
   }
   int i = 0;
   while (next < len) { /* :1408 */
@@ -233,6 +241,12 @@ int or_gso_split(uint8_t *rb, size_t len, or_virtio_hdr hdr,
   return OR_OK;
 }
 
+int or_gso_split(uint8_t *rb, size_t len, or_virtio_hdr hdr,
+                 uint8_t *const *bufs, const size_t *buf_lens, int nbufs,
+                 int *sizes, int offset, int is_v6, int *n_out) {
+  return or_gso_split_cap(rb, len, len, hdr, bufs, buf_lens, nbufs, sizes, offset, is_v6, n_out);
+}
+
 /* Bytes of bufs[i][offset:] one gsoSplit segment touches (gro.go:1419-1488):
  * the packet itself plus fixed-position header writes that may lie past it
  * (IPv4 [2:12), IPv6 [4:6), seq / UDP length at csumStart+4, the flags byte,
@@ -253,10 +267,11 @@ size_t or_gso_split_need(or_virtio_hdr hdr, int is_v6, size_t pkt_len, int last)
   return need;
 }
 
-/* tun/tun.go:514-632 */
-int or_handle_virtio_read(uint8_t *rb, size_t n, uint8_t *const *bufs,
-                          const size_t *buf_lens, int nbufs, int *sizes,
-                          int offset, int *n_out) {
+/* tun/tun.go:514-632; rb[n, cap) is readBuf's spare capacity (Tun.Read
+ * passes tun.readBuf[:n], tun.go:484-503) */
+int or_handle_virtio_read_cap(uint8_t *rb, size_t n, size_t cap, uint8_t *const *bufs,
+                              const size_t *buf_lens, int nbufs, int *sizes,
+                              int offset, int *n_out) {
   *n_out = 0;
   if (n < VNET_LEN) return OR_ERR_SHORT_BUFFER; /* gro.go:84-86 */
   or_virtio_hdr hdr;
@@ -266,7 +281,7 @@ int or_handle_virtio_read(uint8_t *rb, size_t n, uint8_t *const *bufs,
   hdr.gso_size = ne16(rb + 4);
   hdr.csum_start = ne16(rb + 6);
   hdr.csum_offset = ne16(rb + 8);
-  rb += VNET_LEN; n -= VNET_LEN; /* :527 */
+  rb += VNET_LEN; n -= VNET_LEN; cap -= VNET_LEN; /* :527 */
   if (hdr.gso_type == GSO_NONE) { /* :532-556 */
     if (hdr.flags & F_NEEDS_CSUM) {
       int rc = or_gso_none_checksum(rb, n, hdr.csum_start, hdr.csum_offset);
@@ -300,7 +315,13 @@ int or_handle_virtio_read(uint8_t *rb, size_t n, uint8_t *const *bufs,
   if (n < hdr.hdr_len) return OR_ERR_HDR_LEN; /* :615-621 */
   int csum_at = (uint16_t)(hdr.csum_start + hdr.csum_offset);
   if ((size_t)csum_at + 1 >= n) return OR_ERR_CSUM_OFFSET; /* :622-630 */
-  return or_gso_split(rb, n, hdr, bufs, buf_lens, nbufs, sizes, offset, ipv == 6, n_out);
+  return or_gso_split_cap(rb, n, cap, hdr, bufs, buf_lens, nbufs, sizes, offset, ipv == 6, n_out);
+}
+
+int or_handle_virtio_read(uint8_t *rb, size_t n, uint8_t *const *bufs,
+                          const size_t *buf_lens, int nbufs, int *sizes,
+                          int offset, int *n_out) {
+  return or_handle_virtio_read_cap(rb, n, n, bufs, buf_lens, nbufs, sizes, offset, n_out);
 }
 
 /* ====================================================================== */
@@ -742,6 +763,7 @@ static void one_pkt(int mode, uint8_t *arena, const or_pkt *p, const uint64_t *i
       ((uint16_t *)out)[i] = or_checksum(pkt, len, initial ? initial[i] : 0);
       break;
     case 1: { /* L4_FILL: gro.go:1469-1488 with the field treated as zero */
+      if (cs > len) { ((uint16_t *)out)[i] = 0; break; } /* pkt[cs:] panics: 0, no write */
       uint8_t save0 = pkt[at], save1 = pkt[at + 1];
       pkt[at] = 0; pkt[at + 1] = 0;
       uint64_t ph = or_pseudo_header_nofold(pkt + aoff, pkt + aoff + alen, alen, proto,
@@ -753,7 +775,8 @@ static void one_pkt(int mode, uint8_t *arena, const or_pkt *p, const uint64_t *i
       break;
     }
     case 2: /* VALIDATE: checksumValid */
-      ((uint8_t *)out)[i] = (uint8_t)checksum_valid_at(pkt, len, cs, proto, v6); /* u16 iphLen */
+      /* the arena after the packet is its spare capacity; a panic (cs > len) is 0 */
+      ((uint8_t *)out)[i] = (uint8_t)(checksum_valid_at(pkt, len, (size_t)-1, cs, proto, v6) == 1);
       break;
     case 3: { /* PARTIAL: gsoNoneChecksum */
       uint8_t save0 = pkt[at], save1 = pkt[at + 1];

@@ -70,6 +70,10 @@ uint64_t or_pseudo_header_nofold(const uint8_t *src, const uint8_t *dst,
 /* gro.go:554-612 */
 int or_checksum_valid(const uint8_t *pkt, size_t len, uint8_t iph_len,
                       uint8_t proto, int is_v6);
+/* the same with cap(pkt) >= len: the address slices may read pkt[len, cap);
+ * OR_ERR_OUT_OF_RANGE where Go panics (past cap, or iph_len > len) */
+int or_checksum_valid_cap(const uint8_t *pkt, size_t len, size_t cap, uint8_t iph_len,
+                          uint8_t proto, int is_v6);
 /* gro.go:1497-1517 (in place on read_buf) */
 int or_gso_none_checksum(uint8_t *read_buf, size_t len, uint16_t csum_start,
                          uint16_t csum_offset);
@@ -77,12 +81,21 @@ int or_gso_none_checksum(uint8_t *read_buf, size_t len, uint16_t csum_start,
 int or_gso_split(uint8_t *read_buf, size_t len, or_virtio_hdr hdr,
                  uint8_t *const *bufs, const size_t *buf_lens, int nbufs,
                  int *sizes, int offset, int is_v6, int *n_out);
+/* the same with cap(readBuf): read_buf[len, cap) is its spare capacity, which
+ * the pseudo-header address slices may reach (gro.go:1471-1477) */
+int or_gso_split_cap(uint8_t *read_buf, size_t len, size_t cap, or_virtio_hdr hdr,
+                     uint8_t *const *bufs, const size_t *buf_lens, int nbufs,
+                     int *sizes, int offset, int is_v6, int *n_out);
 /* bytes of bufs[i][offset:] a gsoSplit segment of pkt_len bytes writes */
 size_t or_gso_split_need(or_virtio_hdr hdr, int is_v6, size_t pkt_len, int last);
 /* tun/tun.go:514-632.  read_buf starts with the 10-byte virtio header. */
 int or_handle_virtio_read(uint8_t *read_buf, size_t n, uint8_t *const *bufs,
                           const size_t *buf_lens, int nbufs, int *sizes,
                           int offset, int *n_out);
+/* the same with cap(readBuf) >= n (Tun.Read passes tun.readBuf[:n]) */
+int or_handle_virtio_read_cap(uint8_t *read_buf, size_t n, size_t cap, uint8_t *const *bufs,
+                              const size_t *buf_lens, int nbufs, int *sizes,
+                              int offset, int *n_out);
 /* gro.go:1326-1367 (+ tcpGRO/udpGRO/coalesce/apply).  bufs[i] is a Go slice:
  * lens[i] = len(bufs[i]), caps[i] = cap(bufs[i]).  bufs/lens/caps are updated
  * in place (appends grow lens[i]; prepends swap entries), to_write receives

@@ -62,3 +62,54 @@ def fuzz_cases(raw: bool):
             yield vp, nbufs, bufsize, fill, offset, h, bool(rng.integers(0, 2))
         else:
             yield vp, nbufs, bufsize, fill, offset, None, None
+
+
+def short_cases(raw: bool, count: int = 400):
+    """Packets shorter than their pseudo-header addresses (< 20 B IPv4, < 40 B
+    IPv6) whose split still runs, followed by 0-48 bytes of the read buffer's
+    spare capacity: gsoSplit's address slices (gro.go:1471-1477) read the
+    spare bytes, or panic past them.  Yields (buf, n_read, nbufs, bufsize,
+    fill, offset, hdr, is_v6): buf[:n_read] is the read (virtio header first
+    unless raw), buf[n_read:] the spare capacity."""
+    rng = np.random.default_rng(29 + raw)
+    for _ in range(count):
+        v6 = bool(rng.integers(0, 2))
+        plen = int(rng.integers(12, 40 if v6 else 20))
+        pkt = rng.integers(0, 256, plen, dtype=np.uint8)
+        pkt[0] = (0x60 if v6 else 0x45) | (pkt[0] & 0x0F if v6 else 0)
+        tcp = bool(rng.integers(0, 2)) and (raw or v6)
+        cs = int(rng.integers(0, min(plen - 1, 20 if tcp and not raw else plen - 1)))
+        if raw:
+            hdr_len = int(rng.integers(cs, plen))
+        else:
+            hdr_len = cs + 20 if tcp else cs + 8
+            if tcp:
+                if cs + 12 < plen:
+                    pkt[cs + 12] = 0x50
+                else:
+                    tcp = False
+                    hdr_len = cs + 8
+        at = int(rng.integers(0, plen - 1))
+        co = (at - cs) % 65536
+        gso = int(rng.integers(1, 12))
+        gtype = (4 if v6 else 1) if tcp else 5
+        vh = bytes([1, gtype]) + b"".join(int(x).to_bytes(2, "little") for x in (hdr_len, gso, cs, co))
+        spare = rng.integers(0, 256, int(rng.choice([0, 3, 8, 20, 28, 48])), dtype=np.uint8).tobytes()
+        body = pkt.tobytes() if raw else vh + pkt.tobytes()
+        h = (1, gtype, hdr_len, gso, cs, co)
+        yield (body + spare, len(body), 16, int(rng.choice([200, 60])), int(rng.choice([SENT, 0])),
+               int(rng.choice([16, 0, 3])), h if raw else None, v6 if raw else None)
+
+
+def short_valid_cases(count: int = 600):
+    """checksumValid on packets shorter than their addresses (or than iphLen),
+    with 0-40 bytes of spare capacity after them: (buf, n, iph_len, proto,
+    is_v6), the packet being buf[:n] and buf[n:] its spare capacity."""
+    rng = np.random.default_rng(31)
+    for _ in range(count):
+        v6 = bool(rng.integers(0, 2))
+        n = int(rng.integers(0, 48 if v6 else 28))
+        spare = int(rng.choice([0, 1, 4, 12, 24, 40]))
+        buf = rng.integers(0, 256, n + spare, dtype=np.uint8).tobytes()
+        iph = int(rng.choice([0, 8, 20, 40, int(rng.integers(0, 64))]))
+        yield buf, n, iph, int(rng.choice([6, 17, int(rng.integers(0, 256))])), v6

@@ -215,3 +215,46 @@ def test_reference_shaped_single_calls(dev):
     assert dev.gso_none_checksum(rb, 21, 16) is None
     oracle.lib().or_gso_none_checksum((np.frombuffer(rb2, np.uint8)).ctypes.data, len(rb2), 21, 16)
     assert rb == rb2
+
+
+def test_checksum_valid_short_packets_spare_capacity(dev):
+    """checksumValid on packets shorter than their addresses: the per-call
+    form with cap (wgcs_checksum_valid_cap) reads them from the spare bytes
+    or reports OUT_OF_RANGE where Go panics; the batch modes read them from
+    the arena bytes after the packet (include/wgcsum.h), as the oracle does."""
+    import gso_cases
+
+    from wireguard_amd import WgcsError
+
+    cases = list(gso_cases.short_valid_cases())
+    for buf, n, iph, proto, v6 in cases:
+        want = oracle.checksum_valid(buf, iph, proto, v6, n=n)
+        if want is True or want is False:
+            assert dev.checksum_valid(buf, iph, proto, v6, n=n) == want, (n, len(buf), iph, proto, v6)
+        else:
+            with pytest.raises(WgcsError) as ei:
+                dev.checksum_valid(buf, iph, proto, v6, n=n)
+            assert ei.value.code == want
+    rng = np.random.default_rng(12)
+    offs, pos = [], 0
+    for buf, *_ in cases:
+        pos += int(rng.integers(0, 5))
+        offs.append(pos)
+        pos += len(buf)
+    arena = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    for o_, (buf, *_) in zip(offs, cases):
+        arena[o_: o_ + len(buf)] = np.frombuffer(buf, np.uint8)
+    p = _pkts(offs, [c[1] for c in cases], [c[2] for c in cases], 0, [PKT_V6 if c[4] else 0 for c in cases],
+              [c[3] for c in cases])
+    got, want, _, _ = _both(dev, MODE_VALIDATE, arena, p)
+    assert np.array_equal(got, want)
+    # L4_FILL where the checksum field and the addresses lie in the buffer
+    # (gsoSplit's readBuf; no packet reads bytes another one writes)
+    co = np.array([int(rng.integers(0, 8)) for _ in cases])
+    keep = np.array([c[2] + k + 2 <= len(c[0]) and len(c[0]) >= (40 if c[4] else 20) for c, k in zip(cases, co)])
+    assert keep.sum() >= 50
+    p2 = p[keep].copy()
+    p2["csum_offset"] = co[keep]
+    for inplace in (False, True):
+        got, want, ag, ac = _both(dev, MODE_L4_FILL, arena, p2, inplace=inplace)
+        assert np.array_equal(got, want) and np.array_equal(ag, ac)

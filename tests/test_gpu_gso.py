@@ -366,6 +366,82 @@ def test_device_batch_fuzz_geometries(dev, raw):
     assert compared >= 100
 
 
+@pytest.mark.parametrize("raw", [False, True])
+def test_short_packets_spare_capacity(dev, raw):
+    """Packets shorter than their pseudo-header addresses read from a buffer
+    with spare capacity (Tun.Read passes tun.readBuf[:n]): the address slices
+    read the spare bytes (gro.go:1471-1477) or panic past cap -- through the
+    per-call *_cap entry points and through the device batch with
+    WGCS_GSO_JOB_SPARE, every buffer byte for byte against the oracle."""
+    import itertools
+
+    import torch
+
+    from wireguard_amd.tun import GSO_JOB_RAW, GSO_JOB_V6, gso_job_spare
+
+    cases = list(gso_cases.short_cases(raw))
+    ok = 0
+    for buf, n_read, nbufs, bufsize, fill, offset, h, is_v6 in cases:
+        rb_o = np.frombuffer(bytearray(buf), np.uint8).copy()
+        rb_p = rb_o.copy()
+        bo, bp = _bufs(nbufs, bufsize, fill), _bufs(nbufs, bufsize, fill)
+        sz_p = [0] * nbufs
+        if raw:
+            rc_o, n_o, sz_o = oracle.gso_split(rb_o, h, bo, offset, is_v6, n_read=n_read)
+            n_p, err = dev.gso_split(rb_p, VirtioHdr(*h), bp, sz_p, offset, is_v6, n_read=n_read)
+        else:
+            rc_o, n_o, sz_o = oracle.handle_virtio_read(rb_o, bo, offset, n_read=n_read)
+            n_p, err = dev.handle_virtio_read(rb_p, bp, sz_p, offset, n_read=n_read)
+        assert_same((rc_o, n_o, sz_o, bo, rb_o), (_code(err), n_p, sz_p, bp, rb_p), offset=offset, fill=fill)
+        ok += rc_o == 0
+    assert ok >= 100
+    # the same reads as one device batch (fixed slots), spare bytes after each job
+    offs, pos = [], 0
+    for buf, n_read, *_ in cases:
+        offs.append(pos)
+        pos += len(buf) + 3
+    arena = np.zeros(pos + 64, np.uint8)
+    for o_, (buf, *_) in zip(offs, cases):
+        arena[o_: o_ + len(buf)] = np.frombuffer(buf, np.uint8)
+    jobs = np.zeros(len(cases), GSO_JOB_DTYPE)
+    jobs["off"] = offs
+    jobs["len"] = [c[1] + (10 if raw else 0) for c in cases]
+    if raw:  # a raw job's arena bytes are [virtio header | readBuf]: prepend the header
+        arena, pos, offs2 = np.zeros(pos + 64 + 16 * len(cases), np.uint8), 0, []
+        for buf, n_read, nbufs, bufsize, fill, offset, h, is_v6 in cases:
+            vh = bytes([h[0], h[1]]) + b"".join(int(x).to_bytes(2, "little") for x in h[2:])
+            b = vh + buf
+            arena[pos: pos + len(b)] = np.frombuffer(b, np.uint8)
+            offs2.append(pos)
+            pos += len(b) + 3
+        jobs["off"] = offs2
+    jobs["flags"] = [(GSO_JOB_RAW | (GSO_JOB_V6 if c[7] else 0) if raw else 0) | gso_job_spare(len(c[0]) - c[1])
+                     for c in cases]
+    max_segs, stride, offset = 16, 256, 16
+    d_arena = torch.from_numpy(arena).cuda()
+    d_jobs = torch.from_numpy(jobs.view(np.uint8)).cuda()
+    d_out = torch.full((len(cases) * max_segs * stride,), SENT, dtype=torch.uint8, device="cuda")
+    d_sizes = torch.zeros(len(cases) * max_segs, dtype=torch.int32, device="cuda")
+    d_count = torch.zeros(len(cases), dtype=torch.int32, device="cuda")
+    d_status = torch.zeros(len(cases), dtype=torch.int32, device="cuda")
+    dev.gso_split_batch(d_arena, d_jobs, len(cases), d_out, stride, offset, max_segs, d_sizes, d_count, d_status)
+    dev.sync()
+    out = d_out.cpu().numpy().reshape(len(cases), max_segs, stride)
+    count, status = d_count.cpu().numpy(), d_status.cpu().numpy()
+    for j, (buf, n_read, _, _, _, _, h, is_v6) in enumerate(cases):
+        bo = _bufs(max_segs, stride)
+        rb = np.frombuffer(bytearray(buf), np.uint8).copy()
+        if raw:
+            rc, n_o, _ = oracle.gso_split(rb, h, bo, offset, is_v6, n_read=n_read)
+        else:
+            rc, n_o, _ = oracle.handle_virtio_read(rb, bo, offset, n_read=n_read)
+        assert status[j] == rc, (j, status[j], rc)
+        if rc in (0, ERR_TOO_MANY_SEGMENTS):
+            assert count[j] == n_o
+            for i in range(max_segs):
+                assert np.array_equal(out[j, i], bo[i]), (j, i)
+
+
 @pytest.mark.parametrize("v6,udp", [(False, False), (True, False), (False, True)])
 @pytest.mark.parametrize("total,gso", [(65535, 1460), (1500, 1460), (1460, 1460)])
 def test_empty_bufs_split(dev, v6, udp, total, gso):

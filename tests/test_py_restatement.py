@@ -183,3 +183,42 @@ def test_gro_empty_and_invalid_offsets():
     b = [np.zeros(100, np.uint8)]
     assert py.run_handle_gro(b, [5], 16, True)[0] == py.ERR_INVALID_OFFSET
     assert py.run_handle_gro(b, [50], 9, True)[0] == py.ERR_INVALID_OFFSET
+
+
+@pytest.mark.parametrize("raw", [False, True])
+def test_gso_short_packets_spare_capacity(raw):
+    """Packets shorter than their pseudo-header addresses, read from a buffer
+    with spare capacity (tests/gso_cases.py short_cases): both restatements
+    read the addresses from the spare bytes, or panic past cap(readBuf)."""
+    seen = {"compared": 0, "panic": 0}
+    for buf, n_read, nbufs, bufsize, fill, offset, h, is_v6 in gso_cases.short_cases(raw):
+        def run_c(bufs):
+            rb = np.frombuffer(bytearray(buf), np.uint8).copy()
+            if raw:
+                return oracle.gso_split(rb, h, bufs, offset, is_v6, n_read=n_read), rb
+            return oracle.handle_virtio_read(rb, bufs, offset, n_read=n_read), rb
+
+        def run_py(bufs):
+            rb = np.frombuffer(bytearray(buf), np.uint8).copy()
+            if raw:
+                return py.run_gso_split(rb, h, bufs, offset, is_v6, n_read=n_read), rb
+            return py.run_handle_virtio_read(rb, bufs, offset, n_read=n_read), rb
+
+        seen[_gso_compare(run_c, run_py, nbufs, bufsize, fill)] += 1
+    assert seen["compared"] >= 100 and seen["panic"] >= 20, seen
+
+
+def test_checksum_valid_short_packets_spare_capacity():
+    """checksumValid's address slices read up to cap(pkt) (gro.go:558-563):
+    both restatements agree on short packets with spare capacity, including
+    where Go panics (past cap, or iphLen > len)."""
+    seen = {"valid": 0, "invalid": 0, "panic": 0}
+    for buf, n, iph, proto, v6 in gso_cases.short_valid_cases():
+        c = oracle.checksum_valid(buf, iph, proto, v6, n=n)
+        try:
+            p = py.checksum_valid(py.Slice(np.frombuffer(bytearray(buf), np.uint8), 0, n), iph, proto, v6)
+        except py.GoPanic:
+            p = py.ERR_OUT_OF_RANGE
+        assert c == p, (n, len(buf), iph, proto, v6, c, p)
+        seen["panic" if c is not True and c is not False else ("valid" if c else "invalid")] += 1
+    assert seen["panic"] >= 100 and seen["invalid"] >= 100, seen

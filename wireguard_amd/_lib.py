@@ -95,11 +95,16 @@ def load() -> C.CDLL:
         "wgcs_handle_gro_batch": ([vp, vp, vp, vp, u32, vp, vp, vp, vp], i32),
         "wgcs_checksum": ([vp, vp, sz, u64, C.POINTER(C.c_uint16)], i32),
         "wgcs_checksum_valid": ([vp, vp, sz, C.c_uint8, C.c_uint8, i32, C.POINTER(i32)], i32),
+        "wgcs_checksum_valid_cap": ([vp, vp, sz, sz, C.c_uint8, C.c_uint8, i32, C.POINTER(i32)], i32),
         "wgcs_gso_none_checksum": ([vp, vp, sz, C.c_uint16, C.c_uint16], i32),
         "wgcs_checksum_batch_host": ([vp, i32, C.c_uint, vp, sz, vp, vp, u32, vp], i32),
         "wgcs_gso_split": ([vp, vp, sz, C.POINTER(VirtioHdr), u8pp, C.POINTER(sz), i32, C.POINTER(i32), i32, i32,
                             C.POINTER(i32)], i32),
         "wgcs_handle_virtio_read": ([vp, vp, sz, u8pp, C.POINTER(sz), i32, C.POINTER(i32), i32, C.POINTER(i32)], i32),
+        "wgcs_handle_virtio_read_cap": ([vp, vp, sz, sz, u8pp, C.POINTER(sz), i32, C.POINTER(i32), i32,
+                                         C.POINTER(i32)], i32),
+        "wgcs_gso_split_cap": ([vp, vp, sz, sz, C.POINTER(VirtioHdr), u8pp, C.POINTER(sz), i32, C.POINTER(i32), i32,
+                                i32, C.POINTER(i32)], i32),
         "wgcs_handle_gro": ([vp, u8pp, C.POINTER(sz), C.POINTER(sz), i32, i32, i32, C.POINTER(i32), C.POINTER(i32)],
                             i32),
         "wgcs_stager_create": ([vp, u32, u32, sz, u32, u32, C.POINTER(vp)], i32),

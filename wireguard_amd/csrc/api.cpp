@@ -400,21 +400,29 @@ int wgcs_checksum(wgcs_ctx* ctx, const uint8_t* b, size_t n, uint64_t initial, u
 }
 
 // checksumValid(pkt, iphLen, proto, isV6), tun/gro.go:554-612
-int wgcs_checksum_valid(wgcs_ctx* ctx, const uint8_t* pkt, size_t len, uint8_t iph_len, uint8_t proto, int is_v6,
-                        int* valid) {
-  if (!ctx || !valid || (!pkt && len)) return WGCS_ERR_INVALID_ARG;
-  // pkt[srcAddrAt:...+2*addrSize] and pkt[iphLen:] (gro.go:561-562, :611); Go
-  // reaches into a slice's spare capacity for the addresses, which is not an
-  // input this ABI can see, so a packet shorter than its addresses is refused
+// checksumValid(pkt, iphLen, protocol, isV6), tun/gro.go:554-612; pkt[len, cap)
+// is the slice's spare capacity, which the address slices (:558-563) reach
+// for a packet shorter than its addresses.
+int wgcs_checksum_valid_cap(wgcs_ctx* ctx, const uint8_t* pkt, size_t len, size_t cap, uint8_t iph_len, uint8_t proto,
+                            int is_v6, int* valid) {
+  if (!ctx || !valid || (!pkt && cap) || cap < len) return WGCS_ERR_INVALID_ARG;
+  // pkt[srcAddrAt:...+2*addrSize] up to cap, pkt[iphLen:] up to len (gro.go:561-562, :611)
   const size_t need = is_v6 ? 40 : 20;
-  if (len < need || len < iph_len) return set_err(ctx, WGCS_ERR_OUT_OF_RANGE, "packet shorter than its addresses");
+  if (cap < need || len < iph_len)
+    return set_err(ctx, WGCS_ERR_OUT_OF_RANGE, "pkt[%u:] or its addresses past the slice", (unsigned)iph_len);
   if (len >= 0x80000000u) return set_err(ctx, WGCS_ERR_INVALID_ARG, "packet too large");
   wgcs_pkt p;
   wgcs_pkt_set(&p, 0, (uint32_t)len, iph_len, 0, proto, (uint8_t)(is_v6 ? WGCS_PKT_V6 : 0));
   uint8_t v = 0;
-  int rc = wgcs_checksum_batch_host(ctx, WGCS_MODE_VALIDATE, 0, const_cast<uint8_t*>(pkt), len, &p, nullptr, 1, &v);
+  int rc = wgcs_checksum_batch_host(ctx, WGCS_MODE_VALIDATE, 0, const_cast<uint8_t*>(pkt), std::max(len, need), &p,
+                                    nullptr, 1, &v);
   *valid = v;
   return rc;
+}
+
+int wgcs_checksum_valid(wgcs_ctx* ctx, const uint8_t* pkt, size_t len, uint8_t iph_len, uint8_t proto, int is_v6,
+                        int* valid) {
+  return wgcs_checksum_valid_cap(ctx, pkt, len, len, iph_len, proto, is_v6, valid);
 }
 
 // gsoNoneChecksum(readBuf, csumStart, csumOffset), tun/gro.go:1497-1517

@@ -147,8 +147,11 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
       init = (initial && active) ? initial[p] : 0;
     } else if (MODE == WGCS_MODE_L4_FILL || MODE == WGCS_MODE_VALIDATE) {
       r.main_lo = min(cs, len);
-      r.addr_lo = min(v6 ? 8 : 12, len);
-      r.addr_hi = min(v6 ? 40 : 20, len);
+      // the address slices are not bounded by len: a packet shorter than its
+      // addresses has them read from the arena bytes after it, its Go slice's
+      // spare capacity (gro.go:558-563, :1471-1477)
+      r.addr_lo = v6 ? 8 : 12;
+      r.addr_hi = v6 ? 40 : 20;
       if (MODE == WGCS_MODE_L4_FILL) r.fld = fld16;
       pre = (uint32_t)d.proto + ((uint32_t)(len - cs) & 0xFFFFu);  // {0, proto} + BE16(len - iphLen)
     } else if (MODE == WGCS_MODE_PARTIAL) {
@@ -223,15 +226,18 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
     s = fold32_16(s);
     if (((pbase + (uintptr_t)r.main_lo) & 1u) == 0) s = bswap16(s);
     uint32_t t = fold32_16(s + pre + fold64_16(init));  // == the reference's checksum(...)
+    // csum_start past the packet: the reference panics on pkt[iphLen:] (a
+    // batch has no error channel: VALIDATE 0, L4_FILL 0 and no field write)
+    const bool past = (MODE == WGCS_MODE_L4_FILL || MODE == WGCS_MODE_VALIDATE) && cs > len;
     if (sub == 0 && active) {
       if (MODE == WGCS_MODE_VALIDATE) {
-        reinterpret_cast<uint8_t*>(out)[p] = (t == 0xFFFFu) ? 1 : 0;  // ^checksum == 0
+        reinterpret_cast<uint8_t*>(out)[p] = (t == 0xFFFFu && !past) ? 1 : 0;  // ^checksum == 0
       } else if (MODE == WGCS_MODE_FOLD) {
         reinterpret_cast<uint16_t*>(out)[p] = (uint16_t)t;
       } else {
-        const uint16_t c = (uint16_t)~t;
+        const uint16_t c = past ? (uint16_t)0 : (uint16_t)~t;
         reinterpret_cast<uint16_t*>(out)[p] = c;
-        if (inplace && r.fld >= 0 && r.fld + 1 < len) {
+        if (inplace && !past && r.fld >= 0 && r.fld + 1 < len) {
           pkt[r.fld] = (uint8_t)(c >> 8);
           pkt[r.fld + 1] = (uint8_t)c;
         }

@@ -168,14 +168,17 @@ int wgcs_gso_split_batch(wgcs_ctx* ctx, const uint8_t* d_arena, const wgcs_gso_j
   return e == hipSuccess ? WGCS_OK : hip_fail(ctx, e, "gso_split_batch launch");
 }
 
-// gsoSplit(readBuf, hdr, bufs, sizes, offset, isV6) (int, error) -- gro.go:1373
-int wgcs_gso_split(wgcs_ctx* ctx, uint8_t* read_buf, size_t len, const wgcs_virtio_hdr* hdr, uint8_t* const* bufs,
-                   const size_t* buf_lens, int nbufs, int* sizes, int offset, int is_v6, int* n_out) {
-  if (!ctx || !hdr || !n_out || (!read_buf && len)) return WGCS_ERR_INVALID_ARG;
+// gsoSplit(readBuf, hdr, bufs, sizes, offset, isV6) (int, error) -- gro.go:1373;
+// read_buf[len, cap) is readBuf's spare capacity.
+int wgcs_gso_split_cap(wgcs_ctx* ctx, uint8_t* read_buf, size_t len, size_t cap, const wgcs_virtio_hdr* hdr,
+                       uint8_t* const* bufs, const size_t* buf_lens, int nbufs, int* sizes, int offset, int is_v6,
+                       int* n_out) {
+  if (!ctx || !hdr || !n_out || (!read_buf && cap) || cap < len) return WGCS_ERR_INVALID_ARG;
   *n_out = 0;
+  const size_t spare = std::min<size_t>(cap - len, 255);
   int rc;
   std::lock_guard<std::mutex> g(ctx->mu);
-  if ((rc = ensure_pinned(ctx, ctx->h_out, len + 10))) return rc;
+  if ((rc = ensure_pinned(ctx, ctx->h_out, len + spare + 10))) return rc;
   uint8_t* v = (uint8_t*)ctx->h_out.ptr;
   v[0] = hdr->flags;
   v[1] = hdr->gso_type;
@@ -183,10 +186,11 @@ int wgcs_gso_split(wgcs_ctx* ctx, uint8_t* read_buf, size_t len, const wgcs_virt
   memcpy(v + 4, &hdr->gso_size, 2);
   memcpy(v + 6, &hdr->csum_start, 2);
   memcpy(v + 8, &hdr->csum_offset, 2);
-  if (len) memcpy(v + 10, read_buf, len);
+  if (len + spare) memcpy(v + 10, read_buf, len + spare);
   GsoResult r;
-  rc = run_gso_host(ctx, v, len + 10, WGCS_GSO_JOB_RAW | (is_v6 ? WGCS_GSO_JOB_V6 : 0u), bufs, buf_lens, nbufs, sizes,
-                    offset, &r);
+  rc = run_gso_host(ctx, v, len + 10,
+                    WGCS_GSO_JOB_RAW | (is_v6 ? WGCS_GSO_JOB_V6 : 0u) | WGCS_GSO_JOB_SPARE(spare), bufs, buf_lens,
+                    nbufs, sizes, offset, &r);
   if (rc) return rc;
   if (r.status == 0 || r.status == WGCS_ERR_TOO_MANY_SEGMENTS) {
     // the reference zeroes these fields of readBuf before splitting (gro.go:1388,:1393)
@@ -198,17 +202,25 @@ int wgcs_gso_split(wgcs_ctx* ctx, uint8_t* read_buf, size_t len, const wgcs_virt
   return r.status;
 }
 
-// handleVirtioRead(readBuf, bufs, sizes, offset) (int, error) -- tun/tun.go:514
-int wgcs_handle_virtio_read(wgcs_ctx* ctx, uint8_t* read_buf, size_t n, uint8_t* const* bufs, const size_t* buf_lens,
-                            int nbufs, int* sizes, int offset, int* n_out) {
-  if (!ctx || !n_out || (!read_buf && n)) return WGCS_ERR_INVALID_ARG;
+int wgcs_gso_split(wgcs_ctx* ctx, uint8_t* read_buf, size_t len, const wgcs_virtio_hdr* hdr, uint8_t* const* bufs,
+                   const size_t* buf_lens, int nbufs, int* sizes, int offset, int is_v6, int* n_out) {
+  return wgcs_gso_split_cap(ctx, read_buf, len, len, hdr, bufs, buf_lens, nbufs, sizes, offset, is_v6, n_out);
+}
+
+// handleVirtioRead(readBuf, bufs, sizes, offset) (int, error) -- tun/tun.go:514;
+// read_buf[n, cap) is readBuf's spare capacity (Tun.Read passes tun.readBuf[:n]).
+int wgcs_handle_virtio_read_cap(wgcs_ctx* ctx, uint8_t* read_buf, size_t n, size_t cap, uint8_t* const* bufs,
+                                const size_t* buf_lens, int nbufs, int* sizes, int offset, int* n_out) {
+  if (!ctx || !n_out || (!read_buf && cap) || cap < n) return WGCS_ERR_INVALID_ARG;
   *n_out = 0;
+  const size_t spare = std::min<size_t>(cap - n, 255);
   GsoResult r;
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc;
-  if ((rc = ensure_pinned(ctx, ctx->h_out, n + 16))) return rc;
-  if (n) memcpy(ctx->h_out.ptr, read_buf, n);  // the kernel reads it from pinned memory
-  rc = run_gso_host(ctx, (const uint8_t*)ctx->h_out.ptr, n, 0, bufs, buf_lens, nbufs, sizes, offset, &r);
+  if ((rc = ensure_pinned(ctx, ctx->h_out, n + spare + 16))) return rc;
+  if (n + spare) memcpy(ctx->h_out.ptr, read_buf, n + spare);  // the kernel reads it from pinned memory
+  rc = run_gso_host(ctx, (const uint8_t*)ctx->h_out.ptr, n, WGCS_GSO_JOB_SPARE(spare), bufs, buf_lens, nbufs, sizes,
+                    offset, &r);
   if (rc) return rc;
   if (n >= 10 && (r.status == 0 || r.status == WGCS_ERR_TOO_MANY_SEGMENTS)) {
     uint8_t* rb = read_buf + 10;
@@ -229,6 +241,11 @@ int wgcs_handle_virtio_read(wgcs_ctx* ctx, uint8_t* read_buf, size_t n, uint8_t*
   }
   *n_out = r.count;
   return r.status;
+}
+
+int wgcs_handle_virtio_read(wgcs_ctx* ctx, uint8_t* read_buf, size_t n, uint8_t* const* bufs, const size_t* buf_lens,
+                            int nbufs, int* sizes, int offset, int* n_out) {
+  return wgcs_handle_virtio_read_cap(ctx, read_buf, n, n, bufs, buf_lens, nbufs, sizes, offset, n_out);
 }
 
 }  // extern "C"

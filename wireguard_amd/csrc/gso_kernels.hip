@@ -76,6 +76,7 @@ struct Job {
   int count;     // return value n
   int type, flags, ipv;
   int hdr_len, gso, cs, co, plen;
+  int spare;     // bytes of readBuf's spare capacity after the packet (WGCS_GSO_JOB_SPARE)
   int gen;       // 1: byte-granular general path (gso_general_row); 0: the row-streaming fast path
 };
 
@@ -113,8 +114,9 @@ __device__ void count_segments(Job& j, uint32_t out_room, uint32_t max_segs) {
 
 // gsoSplit's own bounds (gro.go:1387-1405 before the loop; :1419-1478 once it
 // runs): an index the Go code would panic on is OUT_OF_RANGE.  Every position
-// is the reference's uint16 sum.  Pseudo-header addresses past len(readBuf)
-// (Go's spare capacity) are refused as well.  Then: does the
+// is the reference's uint16 sum.  The pseudo-header address slices may reach
+// past len(readBuf) into the job's spare capacity (WGCS_GSO_JOB_SPARE), not
+// past it.  Then: does the
 // job fit the row-streaming path (header <= 240 bytes, IP header at least the
 // fixed IPv4 / IPv6 size, checksum field inside the header), or does it take
 // the byte-granular general path?
@@ -127,7 +129,7 @@ __device__ bool split_bounds(Job& j) {
   if (tcp && ((j.cs + 4) & 0xFFFF) + 4 > plen) return false;   // Uint32(readBuf[csumStart+4:])
   if (j.hdr_len < plen) {                                      // the loop runs
     if (j.cs > j.hdr_len) return false;                        // pkt[csumStart:hdrLen]
-    if (plen < (v4 ? 20 : 40)) return false;                   // address slices
+    if (plen + j.spare < (v4 ? 20 : 40)) return false;         // address slices: up to cap(readBuf)
   }
   // (and every per-segment L4 field inside the header: a seq / UDP length /
   // flags byte past hdrLen can land past a short segment's end, which only the
@@ -149,6 +151,7 @@ __device__ Job decode_job(const HdrBytes& hb, uint32_t len, uint32_t jflags, uin
   j.co = (int)hb.le16(8);
   const int plen = (int)len - 10;
   j.plen = plen;
+  j.spare = (int)((jflags >> 8) & 0xFFu);
   if (jflags & WGCS_GSO_JOB_RAW) {  // gsoSplit with the caller's header (gro.go:1373)
     j.ipv = (jflags & WGCS_GSO_JOB_V6) ? 6 : 4;
     if (j.type != GSO_TCPV4 && j.type != GSO_TCPV6) j.type = GSO_UDP_L4;  // protocol choice :1398-1405

@@ -46,6 +46,11 @@ def pkt_off(pkts: np.ndarray) -> np.ndarray:
     return pkts["off_lo"].astype(np.uint64) | (pkts["off_hi"].astype(np.uint64) << np.uint64(32))
 GSO_JOB_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("flags", "<u4")])  # wgcs_gso_job
 GSO_JOB_RAW, GSO_JOB_V6 = 0x1, 0x2  # WGCS_GSO_JOB_*: gsoSplit with the job's own virtio header / isV6
+
+
+def gso_job_spare(n: int) -> int:
+    """WGCS_GSO_JOB_SPARE(n): n bytes of readBuf's spare capacity follow the job in the arena."""
+    return min(n, 255) << 8
 # wgcs_batch (include/wgcsum.h): one batch of wgcs_checksum_batches
 BATCH_DTYPE = np.dtype([("arena", "<u8"), ("pkts", "<u8"), ("initial", "<u8"), ("out", "<u8"), ("n", "<u4"),
                         ("pad", "<u4")])
@@ -224,11 +229,14 @@ class Device:
                                            C.byref(out)))
         return out.value
 
-    def checksum_valid(self, pkt, iph_len: int, proto: int, is_v6: bool) -> bool:
-        """checksumValid(pkt, iphLen, proto, isV6) -- tun/gro.go:554."""
+    def checksum_valid(self, pkt, iph_len: int, proto: int, is_v6: bool, n: int | None = None) -> bool:
+        """checksumValid(pkt, iphLen, proto, isV6) -- tun/gro.go:554.  With n,
+        the packet is pkt[:n] and the rest of pkt its spare capacity."""
         a = _np_u8(bytes(pkt) if not isinstance(pkt, np.ndarray) else pkt)
         v = C.c_int(0)
-        self._check(self.lib.wgcs_checksum_valid(self.h, _ptr(a), len(a), iph_len, proto, int(is_v6), C.byref(v)))
+        ln = len(a) if n is None else n
+        self._check(self.lib.wgcs_checksum_valid_cap(self.h, _ptr(a), ln, len(a), iph_len, proto, int(is_v6),
+                                                     C.byref(v)))
         return bool(v.value)
 
     def gso_none_checksum(self, read_buf, csum_start: int, csum_offset: int):
@@ -245,25 +253,35 @@ class Device:
         lens = (C.c_size_t * len(bufs))(*[len(b) for b in bufs])
         return arr, lens
 
-    def gso_split(self, read_buf, hdr: VirtioHdr, bufs: list, sizes: list, offset: int, is_v6: bool):
-        """gsoSplit(readBuf, hdr, bufs, sizes, offset, isV6) (int, error)."""
+    def gso_split(self, read_buf, hdr: VirtioHdr, bufs: list, sizes: list, offset: int, is_v6: bool,
+                  n_read: int | None = None):
+        """gsoSplit(readBuf, hdr, bufs, sizes, offset, isV6) (int, error).
+        With n_read, readBuf is read_buf[:n_read] and the rest of read_buf its
+        spare capacity (wgcs_gso_split_cap)."""
         a = _np_u8(read_buf)
         arr, lens = self._bufs(bufs)
         csz = (C.c_int * len(bufs))()
         n = C.c_int(0)
-        rc = self.lib.wgcs_gso_split(self.h, _ptr(a), len(a), C.byref(hdr), arr, lens, len(bufs), csz, offset,
-                                     int(is_v6), C.byref(n))
+        nr = len(a) if n_read is None else n_read
+        rc = self.lib.wgcs_gso_split_cap(self.h, _ptr(a), nr, len(a), C.byref(hdr), arr, lens, len(bufs), csz, offset,
+                                         int(is_v6), C.byref(n))
         sizes[: len(bufs)] = list(csz)
         return n.value, self._err(rc)
 
-    def handle_virtio_read(self, read_buf, bufs: list, sizes: list, offset: int):
-        """handleVirtioRead(readBuf, bufs, sizes, offset) (int, error) -- tun/tun.go:514."""
+    def handle_virtio_read(self, read_buf, bufs: list, sizes: list, offset: int, n_read: int | None = None):
+        """handleVirtioRead(readBuf, bufs, sizes, offset) (int, error) -- tun/tun.go:514.
+        With n_read, readBuf is read_buf[:n_read] and the rest of read_buf its
+        spare capacity (Tun.Read's tun.readBuf[:n]; wgcs_handle_virtio_read_cap)."""
         a = _np_u8(read_buf)
         arr, lens = self._bufs(bufs)
         csz = (C.c_int * len(bufs))()
         n = C.c_int(0)
-        rc = self.lib.wgcs_handle_virtio_read(self.h, _ptr(a), len(a), arr, lens, len(bufs), csz, offset,
-                                              C.byref(n))
+        if n_read is None:
+            rc = self.lib.wgcs_handle_virtio_read(self.h, _ptr(a), len(a), arr, lens, len(bufs), csz, offset,
+                                                  C.byref(n))
+        else:
+            rc = self.lib.wgcs_handle_virtio_read_cap(self.h, _ptr(a), n_read, len(a), arr, lens, len(bufs), csz,
+                                                      offset, C.byref(n))
         sizes[: len(bufs)] = list(csz)
         return n.value, self._err(rc)
 
