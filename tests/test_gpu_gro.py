@@ -178,3 +178,12 @@ def test_quirk_calls_host_path(dev):
 
     for pkts, cap, can_udp, lo in quirk_calls():
         run_both(dev, pkts, cap=cap, can_udp=can_udp, lens_override=lo)
+
+
+def test_field_fuzz_host_path(dev):
+    """The header-field fuzz calls (tests/gro_cases.py) through the per-call
+    host path (wgcs_handle_gro)."""
+    import gro_cases
+
+    for pkts, cap, can_udp, lo in gro_cases.field_fuzz_calls(count=60):
+        run_both(dev, pkts, cap=cap, can_udp=can_udp, lens_override=lo)

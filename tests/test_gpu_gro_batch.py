@@ -335,3 +335,13 @@ def test_gro_batch_bench_call_shapes(dev):
 
     calls = [(shape_batch(dev, s), CAP, True, None) for s in CALL_SHAPES]
     assert _check(dev, calls) == len(calls)
+
+
+def test_gro_batch_field_fuzz(dev):
+    """The header-field fuzz calls (tests/gro_cases.py: mutated TOS, TTL,
+    fragment bits, lengths, protocol, TCP flags / data offset / ack / window,
+    UDP length, truncated packets, trailing bytes) in one launch."""
+    import gro_cases
+
+    calls = gro_cases.field_fuzz_calls()
+    assert _check(dev, calls) == len(calls)

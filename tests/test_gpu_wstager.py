@@ -374,3 +374,27 @@ def test_write_stager_quirk_calls(dev):
         assert (0 if err is None else err.code, tw_p) == (rc, tw), k
         assert writes_p == writes, f"call {k}: {_first_diff(writes_p, writes)}"
     ws.close()
+
+
+def test_write_stager_field_fuzz(dev):
+    """The header-field fuzz calls (tests/gro_cases.py) through the write
+    stager, 16 calls per batch, every write(2) image vs the oracle."""
+    import gro_cases
+
+    calls = gro_cases.field_fuzz_calls()
+    ws = WriteStager(dev, depth=2, max_writes=16, max_pkts=16 * 128, max_bytes=16 * 128 * 1600)
+    for lo_k in range(0, len(calls), 16):
+        part = calls[lo_k: lo_k + 16]
+        keep, idxs = [], []
+        for pkts, cap, can_udp, lo in part:
+            bufs, lens = _mk(pkts, cap, OFFSET, lo)
+            keep.append(bufs)
+            idxs.append(ws.push(bufs, lens, OFFSET, can_udp))
+        b = ws.submit()
+        ws.wait(b)
+        for k, (pkts, cap, can_udp, lo) in enumerate(part):
+            rc, tw, writes = _oracle_writes(pkts, cap, can_udp, OFFSET, lo)
+            err, tw_p, writes_p = ws.result(b, idxs[k], len(pkts))
+            assert (0 if err is None else err.code, tw_p) == (rc, tw), lo_k + k
+            assert writes_p == writes, f"call {lo_k + k}: {_first_diff(writes_p, writes)}"
+    ws.close()

@@ -222,3 +222,26 @@ def test_checksum_valid_short_packets_spare_capacity():
         assert c == p, (n, len(buf), iph, proto, v6, c, p)
         seen["panic" if c is not True and c is not False else ("valid" if c else "invalid")] += 1
     assert seen["panic"] >= 100 and seen["invalid"] >= 100, seen
+
+
+def test_gro_field_fuzz_corpus():
+    """The GRO header-field fuzz calls (tests/gro_cases.py): mutated TOS, TTL,
+    fragment bits, lengths, protocol, TCP flags / data offset / ack / window,
+    UDP length, truncation, trailing bytes -- both restatements agree on
+    status, toWrite, slice headers and every buffer byte."""
+    import gro_cases
+    from test_gpu_wstager import _mk
+
+    calls = gro_cases.field_fuzz_calls()
+    merged = writes = 0
+    for c, (pkts, cap, can_udp, lo) in enumerate(calls):
+        bc, lens = _mk(pkts, cap, gro_cases.OFFSET, lo)
+        bp = [b.copy() for b in bc]
+        rc_c, tw_c, order_c, nl_c = oracle.handle_gro(bc, list(lens), gro_cases.OFFSET, can_udp)
+        rc_p, tw_p, order_p, nl_p = py.run_handle_gro(bp, list(lens), gro_cases.OFFSET, can_udp)
+        assert (rc_p, tw_p, order_p, nl_p) == (rc_c, tw_c, order_c, nl_c), c
+        for j in range(len(bc)):
+            assert np.array_equal(bp[j], bc[j]), (c, j)
+        merged += sum(1 for i in range(len(lens)) if nl_c[i] > lens[order_c[i]])
+        writes += len(tw_c)
+    assert merged > 200 and writes > 500, (merged, writes)
