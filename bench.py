@@ -474,15 +474,18 @@ def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, ro
 def strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_events) -> dict:
     """BASELINE.json configs[4]: the seeded 1,048,576 x 1500-B mixed
     TCP4/UDP4/TCP6/UDP6 batch split over the `world` ranks by bytes
-    (shard.make_global_shard; no collective), K launches per rank on one
-    stream (0.27-ms launches at N=1 gain nothing from overlap).  Value =
-    the whole batch's bytes x K / the slowest rank's wall time."""
+    (shard.make_global_shard; no collective), K launches per rank dealt over
+    two streams like the headline's (at N = 8 a rank's launch is ~35 us, and
+    consecutive launches then overlap their ramp and drain; at N = 1 the
+    0.27-ms launches neither gain nor lose).  Value = the whole batch's
+    bytes x K / the slowest rank's wall time."""
     from wireguard_amd import shard
 
     n_cfg, flen, kinds, cfg_idx, _ = CONFIGS["cfg5"]
     arena_np, pkts_np, _, lo, hi = shard.make_global_shard(n_cfg, rank, world, flen, kinds)
     bytes_rank = int(pkts_np["len"].astype(np.int64).sum())
-    leg = checksum_leg(torch, dev, arena_np, pkts_np, mode, args.steps, args.warmup, 1, 2, barrier, use_events,
+    S = 2
+    leg = checksum_leg(torch, dev, arena_np, pkts_np, mode, args.steps, args.warmup, S, 2, barrier, use_events,
                        iso=False, gate=not args.no_gate)
     del arena_np
     elapsed = shard.max_over_ranks(leg["elapsed"], dist, device=red_dev)
@@ -498,11 +501,12 @@ def strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_
         "workload": f"{n_cfg} x {flen}-B {kinds} (25 % each TCP4/UDP4/TCP6/UDP6) frames split by bytes over "
                     f"{world} GPU(s), {MODE_DESC[args.mode]} per step, BASELINE.json configs[{cfg_idx}]",
         "packets_per_rank": [int(x) for x in ranges],
-        "streams": 1,
+        "streams": leg["streams"],
         "rotated_copies": leg["R"],
     }
     if leg["kern_ms"] is not None:
-        out["roofline"] = roofline(kernel_name(mode), bytes_rank, flen, hi - lo, leg["kern_ms"], 1, None, kern_all)
+        out["roofline"] = roofline(kernel_name(mode), bytes_rank, flen, hi - lo, leg["kern_ms"], leg["streams"], None,
+                                   kern_all)
     return out
 
 
