@@ -108,7 +108,8 @@ static inline void wgcs_pkt_set(wgcs_pkt *p, uint64_t off, uint32_t len, uint16_
 #define WGCS_MODE_PARTIAL 3  /* out = ^checksum(pkt[cs:len] field zeroed, BE16(field)) gro.go:1497-1517 */
 #define WGCS_MODE_IP4HDR 4   /* out = ^checksum(pkt[0:cs] with [10:12] zeroed, 0)      gro.go:1134-1138 */
 
-#define WGCS_F_INPLACE 0x1 /* also store the result big-endian into the packet's field */
+#define WGCS_F_INPLACE 0x1 /* also store the result big-endian into the packet's field
+                              (when the field lies inside the packet's len bytes) */
 
 typedef struct wgcs_ctx wgcs_ctx;
 

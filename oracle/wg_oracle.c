@@ -770,7 +770,8 @@ static void one_pkt(int mode, uint8_t *arena, const or_pkt *p, const uint64_t *i
                                             (uint16_t)(len - cs));
       uint16_t c = (uint16_t)~or_checksum(pkt + cs, len - cs, ph);
       ((uint16_t *)out)[i] = c;
-      if (inplace) put_be16(pkt + at, c);
+      /* INPLACE stores into a field inside the packet (WGCS_F_INPLACE) */
+      if (inplace && (size_t)at + 2 <= len) put_be16(pkt + at, c);
       else { pkt[at] = save0; pkt[at + 1] = save1; }
       break;
     }
