@@ -237,7 +237,9 @@ int wgcs_checksum_valid_cap(wgcs_ctx *ctx, const uint8_t *pkt, size_t len, size_
                             uint8_t iph_len, uint8_t proto, int is_v6, int *valid);
 int wgcs_gso_none_checksum(wgcs_ctx *ctx, uint8_t *read_buf, size_t len, uint16_t csum_start,
                            uint16_t csum_offset);
-/* host batch: same semantics as wgcs_checksum_batch on a host arena */
+/* host batch: same semantics as wgcs_checksum_batch on a host arena of
+ * arena_len bytes; VALIDATE / L4_FILL packets whose pseudo-header addresses
+ * would lie past it are refused (OUT_OF_RANGE: the arena is their capacity) */
 int wgcs_checksum_batch_host(wgcs_ctx *ctx, int mode, unsigned flags, uint8_t *h_arena,
                              size_t arena_len, const wgcs_pkt *h_pkts, const uint64_t *h_initial,
                              uint32_t n, void *h_out);

@@ -258,3 +258,22 @@ def test_checksum_valid_short_packets_spare_capacity(dev):
     for inplace in (False, True):
         got, want, ag, ac = _both(dev, MODE_L4_FILL, arena, p2, inplace=inplace)
         assert np.array_equal(got, want) and np.array_equal(ag, ac)
+
+
+def test_host_batch_refuses_addresses_past_the_arena(dev):
+    """wgcs_checksum_batch_host: a VALIDATE / L4_FILL packet whose pseudo-header
+    addresses lie past the host arena (its capacity) is refused with
+    OUT_OF_RANGE, where Go panics; FOLD does not read them."""
+    from wireguard_amd import WgcsError
+    from wireguard_amd._lib import ERR_OUT_OF_RANGE
+
+    arena = np.arange(30, dtype=np.uint8)
+    for mode in (MODE_VALIDATE, MODE_L4_FILL):
+        for flags, n_ok in ((0, 10), (PKT_V6, -10)):  # v4 addresses end at 20, v6 at 40
+            with pytest.raises(WgcsError) as ei:
+                dev.checksum_batch_host(mode, arena.copy(), _pkts([15], [10], 4, 0, flags))
+            assert ei.value.code == ERR_OUT_OF_RANGE
+            if n_ok > 0:  # at offset 10 the v4 addresses end at 30 == the arena's end
+                got = dev.checksum_batch_host(mode, arena.copy(), _pkts([10], [n_ok], 4, 0, flags))
+                assert np.array_equal(got, oracle.checksum_batch(mode, arena.copy(), _pkts([10], [n_ok], 4, 0, flags)))
+    assert dev.checksum_batch_host(MODE_FOLD, arena.copy(), _pkts([25], [5])).shape == (1,)

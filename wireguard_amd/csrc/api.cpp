@@ -339,6 +339,11 @@ int wgcs_checksum_batch_host(wgcs_ctx* ctx, int mode, unsigned flags, uint8_t* h
     const uint64_t off = (uint64_t)h_pkts[i].off_lo | ((uint64_t)h_pkts[i].off_hi << 32);
     if (h_pkts[i].len >= 0x80000000u || off + h_pkts[i].len > arena_len)
       return set_err(ctx, WGCS_ERR_INVALID_ARG, "packet %u outside the arena", i);
+    // VALIDATE / L4_FILL read the pseudo-header addresses whatever len is (a
+    // short packet's spare capacity, include/wgcsum.h): the arena is the cap
+    const size_t addr_end = (h_pkts[i].flags & WGCS_PKT_V6) ? 40 : 20;
+    if ((mode == WGCS_MODE_VALIDATE || mode == WGCS_MODE_L4_FILL) && off + addr_end > arena_len)
+      return set_err(ctx, WGCS_ERR_OUT_OF_RANGE, "packet %u: pseudo-header addresses past the arena", i);
   }
   std::lock_guard<std::mutex> g(ctx->mu);
   hipSetDevice(ctx->device);

@@ -359,7 +359,7 @@ def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int =
     pkts = shape_batch(dev, shape)
     n = len(pkts)
     N = calls * n
-    stride = (CAP + 15) // 16 * 16
+    stride = int(os.environ.get("WGCS_GRO_STRIDE", (CAP + 15) // 16 * 16))  # buffer k at k * stride
     W = (OFFSET + max(len(p) for p in pkts) + 31) // 16 * 16  # bytes restored per buffer
     img = np.zeros((n, W), np.uint8)
     for i, p in enumerate(pkts):
