@@ -1,6 +1,7 @@
 """Per-launch HBM traffic of the path's kernels from rocprofv3 PMC passes.
 
 usage: python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR ALGO_BYTES [KERNEL_SUBSTR] [out.json]
+       [FETCH_PER_BYTE]
 
 FETCH_DIR / WRITE_DIR: `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE`
 output directories of the same bench command (separate passes: FETCH_SIZE
@@ -11,6 +12,11 @@ x 2; hbm_write = WRITE_SIZE x 1024.  KERNEL_SUBSTR (default
 checksum_batch_kernel) picks the kernel; its record is merged into
 profiles/traffic.json under the name the bench line reports
 (wireguard_amd/traffic.py reads it back).
+FETCH_PER_BYTE (default 0.5, the guide's wide-stream value) is what
+FETCH_SIZE x 1024 reports per byte read in the kernel's own access pattern,
+calibrated on a known byte count (scripts/probe_fetch_cal.py): 0.539 for
+gro_batch_kernel's 16-lane rows over packets 64 KiB apart
+(profiles/r4_probe_fetch_cal.json).  read = FETCH_SIZE x 1024 / FETCH_PER_BYTE.
 """
 import csv
 import glob
@@ -55,6 +61,7 @@ def main():
     sub = sys.argv[4] if len(sys.argv) > 4 else "checksum_batch_kernel"
     out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(os.path.dirname(
         os.path.abspath(__file__))), "profiles", "traffic.json")
+    fpb = float(sys.argv[6]) if len(sys.argv) > 6 else 0.5
     fs, ws = counter(fdir, "FETCH_SIZE", sub), counter(wdir, "WRITE_SIZE", sub)
     try:
         with open(out) as f:
@@ -63,12 +70,16 @@ def main():
         res = {}
     new = {}
     for k, v in fs.items():
-        rd = statistics.median(v) * 1024 * 2
+        rd = statistics.median(v) * 1024 / fpb
         wr = statistics.median(ws.get(k, [0.0])) * 1024
         rec = {"hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
                "algorithmic_bytes": algo, "launches": len(v), "kernel": k,
-               "method": "median FETCH_SIZE x1024 x2 (gfx950 half-count) + WRITE_SIZE x1024, separate passes",
+               "method": (f"median FETCH_SIZE x1024 / {fpb} (FETCH per byte of this access pattern"
+                          + (", calibrated: profiles/r4_probe_fetch_cal.json" if fpb != 0.5 else
+                             ", the guide's gfx950 wide-stream half-count") + ") + WRITE_SIZE x1024, separate passes"),
                "source_dirs": [fdir, wdir]}
+        if fpb != 0.5:
+            rec["read_bytes_wide_stream_correction"] = int(statistics.median(v) * 1024 * 2)
         key = bench_key(k)
         # one record per (kernel, launch size): a list once a kernel has several
         old = res.get(key)

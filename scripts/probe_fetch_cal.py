@@ -1,0 +1,37 @@
+"""FETCH_SIZE calibration for gro_batch_kernel's read pattern (NOT product
+code; MI355X_MICROARCH.md: 'other access widths are uncalibrated: calibrate
+on a known byte count in your own access pattern').  Run under
+`rocprofv3 --pmc FETCH_SIZE --kernel-trace`; prints the requested byte counts
+per launch, which scripts/pmc_traffic.py-style parsing divides into."""
+import ctypes
+import json
+import os
+import subprocess
+
+import torch  # first: one HIP runtime per process
+
+here = os.path.dirname(os.path.abspath(__file__))
+so = "/tmp/probe_fetch_cal.so"
+subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-o", so,
+                os.path.join(here, "probe_fetch_cal.hip")], check=True)
+L = ctypes.CDLL(so)
+L.cal_wide_launch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+L.cal_rows_launch.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                              ctypes.c_void_p, ctypes.c_void_p]
+s = torch.cuda.current_stream().cuda_stream
+out = torch.zeros(16, dtype=torch.int32, device="cuda")
+wide_bytes = 384 << 20  # past the 256 MiB Infinity Cache
+wide = torch.ones(wide_bytes, dtype=torch.uint8, device="cuda")
+npk, stride, off = 229376, 65552, 16  # gro_device's 1,792 calls x 128 buffers
+arena = torch.ones(npk * stride + 4096, dtype=torch.uint8, device="cuda")
+rec = {"wide_bytes": wide_bytes, "rows": {}}
+for k in range(5):
+    L.cal_wide_launch(wide.data_ptr(), wide_bytes, out.data_ptr(), s)
+for ln in (1488, 1448, 1500, 60):
+    a0 = [(arena.data_ptr() + p * stride + off) & ~15 for p in range(0, npk)]
+    span = sum(((arena.data_ptr() + p * stride + off + ln + 15) & ~15) - a for p, a in zip(range(npk), a0))
+    rec["rows"][ln] = {"len_bytes": npk * ln, "span_bytes": span}
+    for k in range(5):
+        L.cal_rows_launch(arena.data_ptr(), npk, stride, off, ln, out.data_ptr(), s)
+torch.cuda.synchronize()
+print(json.dumps(rec))
