@@ -22,15 +22,18 @@ s = torch.cuda.current_stream().cuda_stream
 out = torch.zeros(16, dtype=torch.int32, device="cuda")
 wide_bytes = 384 << 20  # past the 256 MiB Infinity Cache
 wide = torch.ones(wide_bytes, dtype=torch.uint8, device="cuda")
-npk, stride, off = 229376, 65552, 16  # gro_device's 1,792 calls x 128 buffers
-arena = torch.ones(npk * stride + 4096, dtype=torch.uint8, device="cuda")
+npk = 229376  # gro_device's 1,792 calls x 128 buffers
+arena = torch.ones(npk * 65552 + 4096, dtype=torch.uint8, device="cuda")
 rec = {"wide_bytes": wide_bytes, "rows": {}}
 for k in range(5):
     L.cal_wide_launch(wide.data_ptr(), wide_bytes, out.data_ptr(), s)
-for ln in (1488, 1448, 1500, 60):
+# (stride, offset, length): gro_device's packets (1,488 B), their payload
+# pieces (1,448), a 1,500-B frame, a 60-B header read, and udp_coalesce's
+# 1,452-B pieces 64 KiB apart
+for stride, off, ln in ((65552, 16, 1488), (65552, 16, 1448), (65552, 16, 1500), (65552, 16, 60), (65536, 0, 1452)):
     a0 = [(arena.data_ptr() + p * stride + off) & ~15 for p in range(0, npk)]
     span = sum(((arena.data_ptr() + p * stride + off + ln + 15) & ~15) - a for p, a in zip(range(npk), a0))
-    rec["rows"][ln] = {"len_bytes": npk * ln, "span_bytes": span}
+    rec["rows"][f"{ln}@{stride}+{off}"] = {"len_bytes": npk * ln, "span_bytes": span}
     for k in range(5):
         L.cal_rows_launch(arena.data_ptr(), npk, stride, off, ln, out.data_ptr(), s)
 torch.cuda.synchronize()
