@@ -338,7 +338,11 @@ int wgcs_stager_wait(wgcs_stager *st, uint64_t batch);
 int wgcs_stager_result(wgcs_stager *st, uint64_t batch, int read_idx, int *status, int *n,
                        const int32_t **sizes, const uint8_t **segs);
 /* copy read r's segments into bufs[i][offset:] exactly as handleVirtioRead
- * leaves them (sizes[], n, ErrTooManySegments / slice-bound checks) */
+ * leaves them (sizes[], n, ErrTooManySegments / slice-bound checks).  `segs`
+ * of wgcs_stager_result holds the packets only: for a read whose header
+ * geometry writes past a segment's end or reads bufs[i][4:6] (an IPv4 header
+ * shorter than 6 bytes), copy_out runs the read again through the per-call
+ * path with these bufs, so that every byte matches (gro.go:1419-1488). */
 int wgcs_stager_copy_out(wgcs_stager *st, uint64_t batch, int read_idx, uint8_t *const *bufs,
                          const size_t *buf_lens, int nbufs, int *sizes, int offset, int *n_out);
 
