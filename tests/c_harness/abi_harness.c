@@ -1,0 +1,138 @@
+/*
+ * abi_harness.c -- TEST INFRASTRUCTURE: the C ABI (include/wgcsum.h) driven
+ * from plain C, the way the cgo shims of INTEGRATION.md call it (no Python,
+ * no torch in the process), checked byte for byte against the CPU oracle
+ * (oracle/wg_oracle.c, linked in as the checker).
+ *
+ *   Tun.Read:  handleVirtioRead (tun/tun.go:514-632) through
+ *              wgcs_handle_virtio_read_cap, with readBuf's spare capacity;
+ *   Tun.Write: handleGRO (tun/gro.go:1326-1367) through wgcs_handle_gro on the
+ *              segments the split produced (they coalesce back);
+ *   checksumValid (gro.go:554-612) through wgcs_checksum_valid_cap on each.
+ *
+ * Exit status 0 and "abi_harness: ok" on success; 1 with a message otherwise.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/wgcsum.h"
+#include "../../oracle/wg_oracle.h"
+
+enum { NBUFS = 128, OFFSET = 16, CAP = 65535 + OFFSET, SPARE = 48 };
+
+static uint32_t lcg = 12345u;
+static uint8_t rnd8(void) { lcg = lcg * 1664525u + 1013904223u; return (uint8_t)(lcg >> 24); }
+
+#define CHECK(cond, ...)                                \
+  do {                                                  \
+    if (!(cond)) {                                      \
+      fprintf(stderr, "abi_harness: FAIL: " __VA_ARGS__); \
+      fprintf(stderr, "\n");                            \
+      return 1;                                         \
+    }                                                   \
+  } while (0)
+
+/* [10-byte virtio header | IPv4 | TCP | payload]: one TCPv4 super-packet
+ * whose split the reference performs (gsoSize 1460). */
+static size_t make_read(uint8_t *rb, size_t total) {
+  memset(rb, 0, total);
+  rb[0] = 1;                              /* VIRTIO_NET_HDR_F_NEEDS_CSUM */
+  rb[1] = 1;                              /* GSO_TCPV4 */
+  rb[2] = 40; rb[3] = 0;                  /* hdrLen (recomputed by handleVirtioRead) */
+  rb[4] = 1460 & 0xFF; rb[5] = 1460 >> 8; /* gsoSize */
+  rb[6] = 20; rb[7] = 0;                  /* csumStart */
+  rb[8] = 16; rb[9] = 0;                  /* csumOffset */
+  uint8_t *ip = rb + 10;
+  const size_t plen = total - 10;
+  ip[0] = 0x45; ip[2] = (uint8_t)(plen >> 8); ip[3] = (uint8_t)plen;
+  ip[4] = 0x12; ip[5] = 0x34; ip[6] = 0x40; ip[8] = 64; ip[9] = 6;
+  for (int k = 12; k < 20; ++k) ip[k] = rnd8();
+  uint8_t *tcp = ip + 20;
+  tcp[0] = 0x0F; tcp[1] = 0xA0; tcp[2] = 0xCA; tcp[3] = 0x6C;
+  for (int k = 4; k < 12; ++k) tcp[k] = rnd8();
+  tcp[12] = 0x50; tcp[13] = 0x18; tcp[14] = 0xFF; tcp[15] = 0xFF;
+  for (size_t k = 40; k < plen; ++k) ip[k] = rnd8();
+  return total;
+}
+
+int main(void) {
+  wgcs_ctx *ctx = NULL;
+  int rc = wgcs_init(0, &ctx);
+  CHECK(rc == WGCS_OK, "wgcs_init: %d (%s)", rc, wgcs_strerror(rc));
+  CHECK(wgcs_abi_version() == WGCS_ABI_VERSION, "ABI version");
+
+  /* ---- Tun.Read: handleVirtioRead with spare capacity after the read ---- */
+  const size_t total = 10 + 65535, cap = total + SPARE;
+  uint8_t *rb_p = malloc(cap), *rb_o = malloc(cap);
+  make_read(rb_p, total);
+  for (size_t k = total; k < cap; ++k) rb_p[k] = rnd8();
+  memcpy(rb_o, rb_p, cap);
+  uint8_t *bp[NBUFS], *bo[NBUFS];
+  size_t lens[NBUFS];
+  for (int i = 0; i < NBUFS; ++i) {
+    bp[i] = malloc(CAP);
+    bo[i] = malloc(CAP);
+    memset(bp[i], 0xA5, CAP);
+    memset(bo[i], 0xA5, CAP);
+    lens[i] = CAP;
+  }
+  int sz_p[NBUFS] = {0}, sz_o[NBUFS] = {0}, n_p = 0, n_o = 0;
+  rc = wgcs_handle_virtio_read_cap(ctx, rb_p, total, cap, bp, lens, NBUFS, sz_p, OFFSET, &n_p);
+  const int rc_o = or_handle_virtio_read_cap(rb_o, total, cap, bo, lens, NBUFS, sz_o, OFFSET, &n_o);
+  CHECK(rc == rc_o && n_p == n_o, "handleVirtioRead: rc %d / %d, n %d / %d", rc, rc_o, n_p, n_o);
+  CHECK(n_p == 45, "handleVirtioRead: %d segments", n_p);
+  CHECK(memcmp(rb_p, rb_o, cap) == 0, "readBuf mutation differs");
+  for (int i = 0; i < NBUFS; ++i) {
+    CHECK(i >= n_p || sz_p[i] == sz_o[i], "size %d", i);
+    CHECK(memcmp(bp[i], bo[i], CAP) == 0, "buffer %d differs", i);
+  }
+
+  /* ---- checksumValid of every segment (any capacity: the buffer's) ---- */
+  for (int i = 0; i < n_p; ++i) {
+    int valid = -1;
+    rc = wgcs_checksum_valid_cap(ctx, bp[i] + OFFSET, (size_t)sz_p[i], CAP - OFFSET, 20, 6, 0, &valid);
+    CHECK(rc == WGCS_OK && valid == 1, "checksumValid segment %d: rc %d valid %d", i, rc, valid);
+    CHECK(or_checksum_valid(bo[i] + OFFSET, (size_t)sz_o[i], 20, 6, 0) == 1, "oracle checksumValid %d", i);
+  }
+
+  /* ---- Tun.Write: handleGRO over the segments (Go slices: len, cap) ---- */
+  size_t gl_p[NBUFS], gc_p[NBUFS], gl_o[NBUFS], gc_o[NBUFS];
+  for (int i = 0; i < n_p; ++i) {
+    gl_p[i] = gl_o[i] = (size_t)(OFFSET + sz_p[i]);
+    gc_p[i] = gc_o[i] = CAP;
+  }
+  int tw_p[NBUFS], tw_o[NBUFS], ntw_p = -1, ntw_o = -1;
+  uint8_t *gp[NBUFS], *go[NBUFS];
+  memcpy(gp, bp, sizeof gp);
+  memcpy(go, bo, sizeof go);
+  rc = wgcs_handle_gro(ctx, gp, gl_p, gc_p, n_p, OFFSET, 1, tw_p, &ntw_p);
+  const int grc = or_handle_gro(go, gl_o, gc_o, n_o, OFFSET, 1, tw_o, &ntw_o);
+  CHECK(rc == grc && ntw_p == ntw_o, "handleGRO: rc %d / %d, writes %d / %d", rc, grc, ntw_p, ntw_o);
+  CHECK(ntw_p >= 1 && ntw_p < n_p, "handleGRO coalesced %d segments into %d writes", n_p, ntw_p);
+  for (int k = 0; k < ntw_p; ++k) CHECK(tw_p[k] == tw_o[k], "toWrite[%d]", k);
+  for (int i = 0; i < n_p; ++i) {
+    /* prepends swap slices (gro.go:696-697): the same permutation on both sides */
+    int j = 0;
+    while (j < n_p && gp[i] != bp[j]) ++j;
+    CHECK(j < n_p && go[i] == bo[j], "slice %d moved differently", i);
+    CHECK(gl_p[i] == gl_o[i] && gc_p[i] == gc_o[i], "slice %d len/cap", i);
+  }
+  for (int i = 0; i < n_p; ++i) CHECK(memcmp(bp[i], bo[i], CAP) == 0, "GRO buffer %d differs", i);
+
+  /* ---- the error contract: a bad mode names itself, per thread ---- */
+  rc = wgcs_checksum_batch(ctx, 99, 0, NULL, NULL, NULL, 1, NULL, NULL);
+  CHECK(rc == WGCS_ERR_INVALID_ARG && strstr(wgcs_last_error(ctx), "99"), "error message: %s", wgcs_last_error(ctx));
+
+  for (int i = 0; i < NBUFS; ++i) {
+    free(bp[i]);
+    free(bo[i]);
+  }
+  free(rb_p);
+  free(rb_o);
+  CHECK(wgcs_destroy(ctx) == WGCS_OK, "wgcs_destroy");
+  printf("abi_harness: ok (handleVirtioRead 45 segments, checksumValid x%d, handleGRO %d writes, bit-exact)\n", n_p,
+         ntw_p);
+  return 0;
+}
