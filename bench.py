@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--mode", default="validate", choices=["validate", "fill"])
     ap.add_argument("--rotate", type=int, default=4, help="distinct batch copies (defeat the 256 MiB MALL)")
     ap.add_argument("--streams", type=int, default=0,
-                    help="launch streams, consecutive batches round-robin (0: 2; 1 for the launch-bound cfg1 and for cfg5, whose 0.26-ms launches gain nothing from overlapping boundaries)")
+                    help="launch streams, consecutive batches round-robin (0: 2; 4 for cfg4; 1 for the launch-bound cfg1 and for cfg5, whose 0.26-ms launches gain nothing from overlapping boundaries)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-event-timing", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end measurement")
@@ -134,7 +134,16 @@ def main():
     if rc is not None:
         sys.exit(rc)
     if args.streams <= 0:
-        args.streams = 1 if args.config in ("cfg1", "cfg5") else 2
+        # cfg4: four launch streams, each on its own hardware queue (below) --
+        # 7.5 us per GSO launch against 7.9 with two (profiles/r4_probe_streams3.jsonl);
+        # the checksum configs are fastest on two
+        args.streams = 1 if args.config in ("cfg1", "cfg5") else (4 if args.config == "cfg4" else 2)
+    # HIP's default of 4 hardware queues per process would put two of the launch
+    # streams on one queue once the context's and torch's streams are counted:
+    # raise it (before HIP initialises) when the streams need more
+    hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    if args.streams + 2 > hwq:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, args.streams + 2)))
     import torch  # before wireguard_amd: one HIP runtime per process
 
     from wireguard_amd import shard, synth

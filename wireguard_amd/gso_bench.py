@@ -9,6 +9,7 @@ Algorithmic bytes per launch = bytes read + bytes written.
 from __future__ import annotations
 
 import json
+import os
 import time
 
 import numpy as np
@@ -135,6 +136,7 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
             "out_align": out_align,
             "in_align": in_align,
             "streams": S,
+            "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             "parallelism": f"shard{world} (no collective)",
         },
         "roofline": {
