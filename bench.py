@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--mode", default="validate", choices=["validate", "fill"])
     ap.add_argument("--rotate", type=int, default=4, help="distinct batch copies (defeat the 256 MiB MALL)")
     ap.add_argument("--streams", type=int, default=0,
-                    help="launch streams, consecutive batches round-robin (0: 2; 4 for cfg4; 1 for the launch-bound cfg1 and for cfg5, whose 0.26-ms launches gain nothing from overlapping boundaries)")
+                    help="launch streams, consecutive batches round-robin (0: 2; 4 for cfg4 and the launch-bound cfg1; 1 for cfg5, whose 0.26-ms launches gain nothing from overlapping boundaries)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-event-timing", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end measurement")
@@ -136,8 +136,10 @@ def main():
     if args.streams <= 0:
         # cfg4: four launch streams, each on its own hardware queue (below) --
         # 7.5 us per GSO launch against 7.9 with two (profiles/r4_probe_streams3.jsonl);
-        # the checksum configs are fastest on two
-        args.streams = 1 if args.config in ("cfg1", "cfg5") else (4 if args.config == "cfg4" else 2)
+        # cfg1's 1.5-MB launches are launch-bound: four streams overlap them, 1.24 us
+        # per launch against 3.23 on one (profiles/r4_probe_cfg1_streams.jsonl); the
+        # 98-MB checksum configs are fastest on two, cfg5's 0.26-ms launches on one
+        args.streams = {"cfg5": 1, "cfg4": 4, "cfg1": 4}.get(args.config, 2)
     # HIP's default of 4 hardware queues per process would put two of the launch
     # streams on one queue once the context's and torch's streams are counted:
     # raise it (before HIP initialises) when the streams need more
