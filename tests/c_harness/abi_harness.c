@@ -8,7 +8,9 @@
  *              wgcs_handle_virtio_read_cap, with readBuf's spare capacity;
  *   Tun.Write: handleGRO (tun/gro.go:1326-1367) through wgcs_handle_gro on the
  *              segments the split produced (they coalesce back);
- *   checksumValid (gro.go:554-612) through wgcs_checksum_valid_cap on each.
+ *   checksumValid (gro.go:554-612) through wgcs_checksum_valid_cap on each;
+ *   the same read through the read stager (push / submit / wait / copy_out)
+ *   and the segments through the write stager (its write(2) images).
  *
  * Exit status 0 and "abi_harness: ok" on success; 1 with a message otherwise.
  */
@@ -69,6 +71,8 @@ int main(void) {
   make_read(rb_p, total);
   for (size_t k = total; k < cap; ++k) rb_p[k] = rnd8();
   memcpy(rb_o, rb_p, cap);
+  uint8_t *rb_pristine = malloc(cap);
+  memcpy(rb_pristine, rb_p, cap);
   uint8_t *bp[NBUFS], *bo[NBUFS];
   size_t lens[NBUFS];
   for (int i = 0; i < NBUFS; ++i) {
@@ -87,6 +91,82 @@ int main(void) {
   for (int i = 0; i < NBUFS; ++i) {
     CHECK(i >= n_p || sz_p[i] == sz_o[i], "size %d", i);
     CHECK(memcmp(bp[i], bo[i], CAP) == 0, "buffer %d differs", i);
+  }
+
+  /* the split's segments, kept for the stager checks below */
+  uint8_t *seg[NBUFS];
+  for (int i = 0; i < NBUFS; ++i) {
+    seg[i] = malloc(CAP);
+    memcpy(seg[i], bo[i], CAP);
+  }
+
+  /* ---- Tun.Read through the read stager: push, submit, wait, copy_out ---- */
+  {
+    wgcs_stager *st = NULL;
+    rc = wgcs_stager_create(ctx, 2, 4, 4 * (total + 64), NBUFS, CAP - OFFSET, &st);
+    CHECK(rc == WGCS_OK, "wgcs_stager_create: %d", rc);
+    int idx = -1;
+    uint64_t batch = 0;
+    CHECK(wgcs_stager_push(st, rb_pristine, total, &idx) == WGCS_OK && idx == 0, "stager push");
+    CHECK(wgcs_stager_submit(st, &batch) == WGCS_OK && wgcs_stager_wait(st, batch) == WGCS_OK, "stager submit/wait");
+    uint8_t *sb[NBUFS];
+    int ssz[NBUFS] = {0}, sn = 0;
+    for (int i = 0; i < NBUFS; ++i) {
+      sb[i] = malloc(CAP);
+      memset(sb[i], 0xA5, CAP);
+    }
+    rc = wgcs_stager_copy_out(st, batch, 0, sb, lens, NBUFS, ssz, OFFSET, &sn);
+    CHECK(rc == WGCS_OK && sn == n_o, "stager copy_out: rc %d n %d", rc, sn);
+    for (int i = 0; i < NBUFS; ++i) {
+      CHECK(i >= sn || ssz[i] == sz_o[i], "stager size %d", i);
+      CHECK(memcmp(sb[i], seg[i], CAP) == 0, "stager buffer %d differs", i);
+      free(sb[i]);
+    }
+    CHECK(wgcs_stager_destroy(st) == WGCS_OK, "stager destroy");
+  }
+
+  /* ---- Tun.Write through the write stager: the write(2) images ---- */
+  {
+    wgcs_wstager *ws = NULL;
+    rc = wgcs_wstager_create(ctx, 2, 4, 4 * NBUFS, 4 * NBUFS * 1600, &ws);
+    CHECK(rc == WGCS_OK, "wgcs_wstager_create: %d", rc);
+    size_t wl[NBUFS], wc[NBUFS], ol[NBUFS], oc[NBUFS];
+    uint8_t *wb[NBUFS], *ob[NBUFS];
+    for (int i = 0; i < n_o; ++i) {
+      wb[i] = malloc(CAP);
+      ob[i] = malloc(CAP);
+      memcpy(wb[i], seg[i], CAP);
+      memcpy(ob[i], seg[i], CAP);
+      wl[i] = ol[i] = (size_t)(OFFSET + sz_o[i]);
+      wc[i] = oc[i] = CAP;
+    }
+    int widx = -1;
+    uint64_t wbatch = 0;
+    rc = wgcs_wstager_push(ws, (const uint8_t *const *)wb, wl, wc, n_o, OFFSET, 1, &widx);
+    CHECK(rc == WGCS_OK && widx == 0, "wstager push: %d", rc);
+    CHECK(wgcs_wstager_submit(ws, &wbatch) == WGCS_OK && wgcs_wstager_wait(ws, wbatch) == WGCS_OK, "wstager submit/wait");
+    int wst = -1, nw = -1, wtw[NBUFS];
+    const uint8_t *imgs[NBUFS];
+    size_t ilen[NBUFS];
+    rc = wgcs_wstager_result(ws, wbatch, widx, &wst, &nw, wtw, imgs, ilen);
+    int otw[NBUFS], onw = -1;
+    uint8_t *obp[NBUFS];
+    memcpy(obp, ob, sizeof(uint8_t *) * (size_t)n_o);
+    const int orc = or_handle_gro(obp, ol, oc, n_o, OFFSET, 1, otw, &onw);
+    CHECK(rc == WGCS_OK && wst == orc && nw == onw, "wstager result: rc %d status %d/%d writes %d/%d", rc, wst, orc,
+          nw, onw);
+    for (int k = 0; k < nw; ++k) {
+      const int i = otw[k];
+      CHECK(wtw[k] == i, "wstager toWrite[%d]", k);
+      /* the write(2) image: the virtio header and the packet, bufs[i][offset-10:len] */
+      CHECK(ilen[k] == ol[i] - (OFFSET - 10) && memcmp(imgs[k], obp[i] + OFFSET - 10, ilen[k]) == 0,
+            "wstager image %d differs", k);
+    }
+    CHECK(wgcs_wstager_destroy(ws) == WGCS_OK, "wstager destroy");
+    for (int i = 0; i < n_o; ++i) {
+      free(wb[i]);
+      free(ob[i]);
+    }
   }
 
   /* ---- checksumValid of every segment (any capacity: the buffer's) ---- */
@@ -128,11 +208,13 @@ int main(void) {
   for (int i = 0; i < NBUFS; ++i) {
     free(bp[i]);
     free(bo[i]);
+    free(seg[i]);
   }
+  free(rb_pristine);
   free(rb_p);
   free(rb_o);
   CHECK(wgcs_destroy(ctx) == WGCS_OK, "wgcs_destroy");
-  printf("abi_harness: ok (handleVirtioRead 45 segments, checksumValid x%d, handleGRO %d writes, bit-exact)\n", n_p,
-         ntw_p);
+  printf("abi_harness: ok (handleVirtioRead 45 segments, read stager, write stager, checksumValid x%d, handleGRO %d "
+         "writes, bit-exact)\n", n_p, ntw_p);
   return 0;
 }
