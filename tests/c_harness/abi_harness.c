@@ -10,7 +10,8 @@
  *              segments the split produced (they coalesce back);
  *   checksumValid (gro.go:554-612) through wgcs_checksum_valid_cap on each;
  *   the same read through the read stager (push / submit / wait / copy_out)
- *   and the segments through the write stager (its write(2) images).
+ *   and the segments through the write stager (its write(2) images);
+ *   conn: splitMessages (conn/bind.go:542-597) on a recvmmsg batch.
  *
  * Exit status 0 and "abi_harness: ok" on success; 1 with a message otherwise.
  */
@@ -201,6 +202,54 @@ int main(void) {
   }
   for (int i = 0; i < n_p; ++i) CHECK(memcmp(bp[i], bo[i], CAP) == 0, "GRO buffer %d differs", i);
 
+  /* ---- conn: splitMessages on a recvmmsg batch (2 UDP_GRO datagrams) ---- */
+  {
+    enum { NM = 128, FIRST = 126, BL = 65535, SEG = 1452, NSEG = 45 };
+    uint8_t *mp[NM], *mo[NM], cm[NM][24];
+    const uint8_t *oobs[NM];
+    size_t nns[NM];
+    int ns_p[NM], ns_o[NM], asrc[NM];
+    or_msg msgs[NM];
+    for (int i = 0; i < NM; ++i) {
+      mp[i] = malloc(BL);
+      mo[i] = malloc(BL);
+      for (int k = 0; k < BL; ++k) mp[i][k] = rnd8();
+      memcpy(mo[i], mp[i], BL);
+      memset(cm[i], 0, sizeof cm[i]);
+      nns[i] = 0;
+      ns_p[i] = ns_o[i] = 0;
+      if (i >= FIRST) { /* a UDP_GRO cmsg {Len 18, SOL_UDP 17, UDP_GRO 104, gso} (conn/gso.go:55-64) */
+        const uint64_t hl = 18;
+        const int32_t lvl = 17, typ = 104;
+        const uint16_t g = SEG;
+        memcpy(cm[i], &hl, 8);
+        memcpy(cm[i] + 8, &lvl, 4);
+        memcpy(cm[i] + 12, &typ, 4);
+        memcpy(cm[i] + 16, &g, 2);
+        nns[i] = 24;
+        ns_p[i] = ns_o[i] = SEG * NSEG;
+      }
+      oobs[i] = cm[i];
+      msgs[i].buf = mo[i];
+      msgs[i].buf_len = msgs[i].buf_cap = BL;
+      msgs[i].n = ns_o[i];
+      msgs[i].oob = cm[i];
+      msgs[i].oob_len = msgs[i].oob_cap = 24;
+      msgs[i].nn = (int)nns[i];
+      msgs[i].addr = i;
+    }
+    int np_p = -1, np_o = -1;
+    rc = wgcs_split_messages(ctx, mp, BL, ns_p, oobs, nns, NM, FIRST, asrc, &np_p);
+    const int src = or_split_messages(msgs, NM, FIRST, &np_o);
+    CHECK(rc == src && np_p == np_o && np_p == 2 * NSEG, "splitMessages: rc %d / %d, n %d / %d", rc, src, np_p, np_o);
+    for (int i = 0; i < NM; ++i) {
+      CHECK(ns_p[i] == msgs[i].n && asrc[i] == msgs[i].addr, "splitMessages msg %d", i);
+      CHECK(memcmp(mp[i], mo[i], BL) == 0, "splitMessages buffer %d differs", i);
+      free(mp[i]);
+      free(mo[i]);
+    }
+  }
+
   /* ---- the error contract: a bad mode names itself, per thread ---- */
   rc = wgcs_checksum_batch(ctx, 99, 0, NULL, NULL, NULL, 1, NULL, NULL);
   CHECK(rc == WGCS_ERR_INVALID_ARG && strstr(wgcs_last_error(ctx), "99"), "error message: %s", wgcs_last_error(ctx));
@@ -215,6 +264,6 @@ int main(void) {
   free(rb_o);
   CHECK(wgcs_destroy(ctx) == WGCS_OK, "wgcs_destroy");
   printf("abi_harness: ok (handleVirtioRead 45 segments, read stager, write stager, checksumValid x%d, handleGRO %d "
-         "writes, bit-exact)\n", n_p, ntw_p);
+         "writes, splitMessages 90 packets, bit-exact)\n", n_p, ntw_p);
   return 0;
 }
