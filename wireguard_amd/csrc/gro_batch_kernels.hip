@@ -506,48 +506,95 @@ struct Planner {
     return result;
   }
 
-  // run_flow for a long TCP flow, by a whole wave (f wave-uniform): lane 0
-  // walks the packets and takes the in-order append fast path; a packet that
-  // leaves it goes through tcp_gro_wave (one lane per item).
-  __device__ void run_flow_wave(int f, int lane) {
+  // tcp_append_fast for a whole wave: the flow's packets from bi on, 64
+  // packet indices at a time (lane k: packet w + k, a member of the flow when
+  // its flow id is f -- a flow's packets are in index order).  Every member
+  // evaluates tcp_append_fast's checks against the item as it would be after
+  // each earlier member of the run had appended: numMerged grows by one per
+  // member, and since a member only appends when the one before it left a
+  // multiple of gsoSize without PSH, every earlier member's payload was
+  // gsoSize.  So the first member whose checks fail is exactly the packet at
+  // which the one-lane walk leaves the fast path, and every member before it
+  // appends -- all at once, each lane linking its own piece.  Returns that
+  // packet (kNone: the flow's remaining packets all appended).  c is
+  // wave-uniform.
+  __device__ int tcp_append_run(TailCache& c, int f, int bi, int n_eff, int lane) {
+    if (c.it == kNone) return bi;
+    for (int w = bi; w < n_eff; w += 64) {  // wave-uniform
+      const int q = w + lane;
+      const bool mem = q < n_eff && S.cand[q] != C_NOT && !S.noop[q] && S.flow[q] == f;
+      const uint64_t M = __ballot(mem);
+      if (!M) continue;
+      const uint64_t Mb = M & ((1ull << lane) - 1ull);
+      const int rank = __builtin_popcountll(Mb);
+      const int prev = Mb ? 63 - __builtin_clzll(Mb) : lane;  // the member before (lane: none in this window)
+      uint4 R = make_uint4(0, 0, 0, 0);
+      if (mem) R = S.rec[q];
+      const uint32_t gso = R.z & 0xFFFFu, pshb = (R.w >> 16) & 1u, th = R.w & 0xFFu;
+      const uint32_t gso_prev = (uint32_t)__shfl((int)gso, prev), psh_prev = (uint32_t)__shfl((int)pshb, prev);
+      const bool first = Mb == 0;
+      const uint32_t nm = c.nm + (uint32_t)rank;
+      const uint32_t slen = c.slen + (uint32_t)rank * c.g;
+      const uint16_t lhs = (uint16_t)(c.g + (uint16_t)(c.g * nm));
+      const bool psh = first ? c.psh != 0 : psh_prev != 0;
+      const bool mult = first ? c.mult : gso_prev == c.g;
+      const bool ok = th == c.l4h && th <= 20 && R.y == c.ipattr && R.x == c.seq + (uint32_t)lhs && !psh && mult &&
+                      gso <= c.g && (int)c.cap - offset >= ((int)slen - offset) + (int)gso && (nm != 0 || c.valid_s) &&
+                      ((R.w >> 24) & 1u);
+      const uint64_t fail = __ballot(mem && !ok);
+      const uint64_t A = fail ? M & ((1ull << __builtin_ctzll(fail)) - 1ull) : M;
+      if ((A >> lane) & 1ull) {
+        S.pstart[q] = (uint16_t)(c.iphit + c.l4h);
+        S.plen[q] = (uint16_t)gso;  // S.pnext[q] is kNone since step 1
+        S.pnext[first ? c.stail : w + prev] = (int16_t)q;
+        S.res[q] = R_COALESCED;
+      }
+      if (A) {  // the item after the run (only its last member may carry PSH or a short payload)
+        const int L = 63 - __builtin_clzll(A);
+        const int cnt = __builtin_popcountll(A);
+        const uint32_t gl = (uint32_t)__shfl((int)gso, L), pl = (uint32_t)__shfl((int)pshb, L);
+        c.stail = w + L;
+        c.scount += cnt;
+        c.slen += (uint32_t)(cnt - 1) * c.g + gl;
+        c.nm += (uint32_t)cnt;
+        c.mult = gl == c.g;
+        c.dirty = true;
+        if (pl) {  // pktHead[iphLen+13] |= PSH (gro.go:724-729)
+          if (lane == 0) {
+            S.it_psh[c.it] = 1;
+            S.spsh[c.s] = 1;
+          }
+          c.psh = 1;
+        }
+      }
+      if (fail) return w + __builtin_ctzll(fail);
+    }
+    return kNone;
+  }
+
+  // run_flow for a long TCP flow, by a whole wave (f wave-uniform): runs of
+  // in-order appends go through tcp_append_run; a packet that leaves it goes
+  // through tcp_gro_wave (one lane per item).
+  __device__ void run_flow_wave(int f, int n_eff, int lane) {
     TailCache c;
     c.it = kNone;
     c.dirty = false;
-    bool fresh = false;
-    uint4 R = S.rec[f];
     bool try_fast = true;
     for (int i = f; i != kNone;) {  // wave-uniform
-      const int nx = (int)(int16_t)(R.z >> 16);
-      const uint4 Rn = nx != kNone ? S.rec[nx] : R;  // the next record, a step ahead
-      int fast = 0;
-      if (lane == 0 && try_fast) {
-        if (!fresh) {
-          load_tail(c, f);
-          fresh = true;
-        }
-        fast = tcp_append_fast(c, i, R) ? 1 : 0;
-        if (fast) {
-          S.res[i] = R_COALESCED;
-        } else {
-          flush_tail(c);
-          c = TailCache{};  // reloaded after the item loop: nothing of it lives across that
-          c.it = kNone;
-          fresh = false;
-        }
+      if (try_fast) {
+        load_tail(c, f);
+        i = tcp_append_run(c, f, i, n_eff, lane);
+        if (lane == 0) flush_tail(c);  // the item loop below reads the item from LDS
+        c.dirty = false;
+        if (i == kNone) break;
       }
-      fast = __builtin_amdgcn_readfirstlane(fast);
       // in a reordered flow the in-order fast path is tried again only after
-      // it last succeeded or the item loop appended to the flow's last item
-      try_fast = fast != 0;
-      if (!fast) {
-        const int res = tcp_gro_wave(i, f, lane);
-        try_fast = res == R_COALESCED && S.fl_tail[f] != kNone && S.stail[S.it_slot[S.fl_tail[f]]] == i;
-        if (lane == 0) S.res[i] = (uint8_t)res;
-      }
-      i = nx;
-      R = Rn;
+      // the item loop appended to the flow's last item
+      const int res = tcp_gro_wave(i, f, lane);
+      try_fast = res == R_COALESCED && S.fl_tail[f] != kNone && S.stail[S.it_slot[S.fl_tail[f]]] == i;
+      if (lane == 0) S.res[i] = (uint8_t)res;
+      i = S.fnext[i];
     }
-    if (lane == 0) flush_tail(c);
   }
 
   // apply{TCP,UDP}Coalesce (gro.go:1364-1366) for item `it`, or -- after
@@ -903,11 +950,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
                      (uint32_t)S.th[t] | ((uint32_t)S.iph[t] << 8) | ((uint32_t)S.psh[t] << 16) |
                          ((uint32_t)S.valid[t] << 24));
   if (live) S.rec[t] = rec;  // step 2's key-word reads ended at the barrier above
-  // a TCP flow of kCoopMin or more packets with two or more links that
-  // neither append nor prepend (so they build up several items) is walked by a whole wave
-  // (its item loop one lane per item, run_flow_wave); the others by one thread
+  // a TCP flow of kCoopMin or more packets is walked by a whole wave (its
+  // in-order runs 64 packets at a time, its item loop one lane per item,
+  // run_flow_wave); the others by one thread
   const bool leader = live && S.flow[t] == t;
-  const bool coop = leader && S.cand[t] <= C_TCP6 && S.fsize[t] >= (uint32_t)kCoopMin && S.fooo[t] >= 2u;
+  const bool coop = leader && S.cand[t] <= C_TCP6 && S.fsize[t] >= (uint32_t)kCoopMin;
   if (coop) {
     S.coop[atomicAdd(&S.n_coop, 1)] = (int16_t)t;
     S.fbase[t] = (int16_t)atomicAdd(&S.fitem_top, (int)S.fsize[t]);  // room for one item per packet
@@ -917,7 +964,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
   const bool raw = n_eff < n;  // "invalid offset": coalescing happened, apply* did not
   Planner P{S, arena, offset};
   if (leader && !coop) P.run_flow(t);
-  for (int k = wv; k < S.n_coop; k += 4) P.run_flow_wave(S.coop[k], lane);  // wave-uniform
+  for (int k = wv; k < S.n_coop; k += 4) P.run_flow_wave(S.coop[k], n_eff, lane);  // wave-uniform
   __syncthreads();
 #ifdef WGCS_GRO_STAMPS
   stp[3] = __builtin_amdgcn_s_memrealtime();
