@@ -77,13 +77,12 @@ struct GroSmem {
   // long TCP flows walked by a whole wave (Planner::run_flow_wave): the flow's
   // packet count, its items as an array (fitem[fbase[f] .. fbase[f] + fnit[f])
   // in insertion order), the list of such flows
-  uint32_t fsize[kMaxB], fooo[kMaxB];  // packets of the flow, and its links that neither append nor prepend
+  uint32_t fsize[kMaxB];  // packets of the flow
   int16_t fbase[kMaxB], fnit[kMaxB], fitem[kMaxB], coop[kMaxB];
   int n_eff, n_write, n_mat, n_coop, fitem_top;
 };
 
 __device__ __forceinline__ uint32_t be16g(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
-__device__ __forceinline__ uint32_t be32g(const uint8_t* p) { return (be16g(p) << 16) | be16g(p + 2); }
 
 __device__ __forceinline__ uint32_t fnv(uint32_t h, uint32_t b) { return (h ^ b) * 16777619u; }
 
@@ -776,7 +775,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
     S.it_alive[t] = 0;
     S.ndst[t] = kNone;
     S.fsize[t] = 0;
-    S.fooo[t] = 0;
   }
   // groCandidate + the tcpGRO / udpGRO checks that return groResultNoop
   if (t < n_eff) {
@@ -891,7 +889,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
   // ---- 2. flow ids (first earlier packet with the same key in the same table)
   if (t < n_eff && S.cand[t] != C_NOT && !S.noop[t]) {
     const uint8_t c = S.cand[t];
-    const bool v6 = c == C_TCP6 || c == C_UDP6, tcp = c <= C_TCP6;
+    const bool v6 = c == C_TCP6 || c == C_UDP6;
     const int nkw = v6 ? 10 : 4;  // key words: the class fixes the layout (ack is 0 for UDP)
     const uint32_t kh = S.keyh[t];
     int f = t;
@@ -919,11 +917,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
       }
     }
     S.fnext[t] = (int16_t)nx;
-    // a TCP packet whose successor in the flow neither continues its sequence
-    // (an append) nor ends right before it (a prepend): reordering that builds
-    // up several items of the flow, which tcpGRO's item loop then scans
-    if (tcp && nx != kNone && S.seq[nx] != S.seq[t] + S.gso[t] && S.seq[nx] + S.gso[nx] != S.seq[t])
-      atomicAdd(&S.fooo[f], 1u);
   }
   // checksumValid of every candidate: one 16-lane row per packet
   for (int p = row; p < n_eff; p += 16) {  // row-uniform
