@@ -70,6 +70,7 @@ struct GroSmem {
   int16_t m_buf[kMaxB], m_first[kMaxB], m_count[kMaxB], m_item[kMaxB];
   uint8_t m_psh[kMaxB];
   uint8_t cand[kMaxB], noop[kMaxB], iph[kMaxB], th[kMaxB], psh[kMaxB], valid[kMaxB], spsh[kMaxB], szero[kMaxB];
+  uint8_t swalk[kMaxB];  // slot s's pieces moved since they were appended (a prepend): finish_item walks them
   uint8_t it_iph[kMaxB], it_l4h[kMaxB], it_psh[kMaxB], it_bad[kMaxB], it_alive[kMaxB], it_cand[kMaxB];
   uint8_t res[kMaxB];                   // groResult of each packet (R_*)
   int16_t ndst[kMaxB];                  // piece p's destination buffer in its final item (-1: none)
@@ -211,6 +212,7 @@ struct Planner {
       t16 = S.stail[s]; S.stail[s] = S.stail[bi]; S.stail[bi] = t16;
       t8 = S.spsh[s]; S.spsh[s] = S.spsh[bi]; S.spsh[bi] = t8;
       t16 = S.scount[s]; S.scount[s] = S.scount[bi]; S.scount[bi] = t16;
+      S.swalk[s] = 1;  // every piece now sits behind the new head
     } else {
       if ((int)S.bcap[S.sbuf[s]] - offset < new_len) return CR_INSUFF;
       if (S.it_nm[it] == 0 && !S.valid[s]) return CR_ITEM_BAD;
@@ -222,6 +224,8 @@ struct Planner {
       S.pstart[bi] = (uint16_t)hdrs;
       S.plen[bi] = (uint16_t)pay;
       S.pnext[bi] = kNone;
+      S.ndst[bi] = S.sbuf[s];  // its place in the item's buffer: behind everything before it
+      S.npos[bi] = S.slen[s] - (uint32_t)offset;
       S.pnext[S.stail[s]] = (int16_t)bi;
       S.stail[s] = (int16_t)bi;
       S.scount[s]++;
@@ -254,7 +258,7 @@ struct Planner {
   // The flow's last item, cached in registers for the in-order append fast
   // path below (it = kNone: nothing cached / no item).
   struct TailCache {
-    int it, s, tgt, stail, scount;
+    int it, s, tgt, stail, scount, buf;
     uint32_t l4h, iphit, ipattr, g, nm, seq, psh, slen, cap, valid_s;
     bool dirty;  // running fields newer than LDS
     bool mult;   // the item's payload is a multiple of its gsoSize
@@ -274,6 +278,7 @@ struct Planner {
     c.psh = S.it_psh[it];
     const int s = c.s;
     c.tgt = S.shead[s];
+    c.buf = S.sbuf[s];
     c.slen = S.slen[s];
     c.cap = S.bcap[S.sbuf[s]];
     c.valid_s = S.valid[s];
@@ -317,6 +322,8 @@ struct Planner {
     }
     S.pstart[bi] = (uint16_t)(c.iphit + c.l4h);
     S.plen[bi] = (uint16_t)pay;  // S.pnext[bi] is kNone since step 1
+    S.ndst[bi] = (int16_t)c.buf;
+    S.npos[bi] = c.slen - (uint32_t)offset;
     S.pnext[c.stail] = (int16_t)bi;
     c.stail = bi;
     ++c.scount;
@@ -362,6 +369,8 @@ struct Planner {
         S.pstart[bi] = (uint16_t)hdrs;
         S.plen[bi] = (uint16_t)pay;
         S.pnext[bi] = kNone;
+        S.ndst[bi] = S.sbuf[s];
+        S.npos[bi] = S.slen[s] - (uint32_t)offset;
         S.pnext[S.stail[s]] = (int16_t)bi;
         S.stail[s] = (int16_t)bi;
         S.scount[s]++;
@@ -545,6 +554,8 @@ struct Planner {
       if ((A >> lane) & 1ull) {
         S.pstart[q] = (uint16_t)(c.iphit + c.l4h);
         S.plen[q] = (uint16_t)gso;  // S.pnext[q] is kNone since step 1
+        S.ndst[q] = (int16_t)c.buf;
+        S.npos[q] = slen - (uint32_t)offset;
         S.pnext[first ? c.stail : w + prev] = (int16_t)q;
         S.res[q] = R_COALESCED;
       }
@@ -606,12 +617,16 @@ struct Planner {
       if (!raw) S.szero[s] = 1;  // numMerged == 0: empty virtioNetHdr (:1168-1174, :1250-1256)
       return;
     }
-    // the item's pieces go behind its head packet: one row each (step 4)
-    uint32_t pos = S.plen[h];
-    for (int p = S.pnext[h]; p != kNone; p = S.pnext[p]) {
-      S.ndst[p] = S.sbuf[s];
-      S.npos[p] = pos;
-      pos += S.plen[p];
+    // the item's pieces go behind its head packet: one row each (step 4).
+    // Every append placed its piece already (ndst / npos); only after a
+    // prepend, which puts a new head before them all, are they placed again
+    if (S.swalk[s]) {
+      uint32_t pos = S.plen[h];
+      for (int p = S.pnext[h]; p != kNone; p = S.pnext[p]) {
+        S.ndst[p] = S.sbuf[s];
+        S.npos[p] = pos;
+        pos += S.plen[p];
+      }
     }
     materialize(S.sbuf[s], kNone, 0, 0, S.spsh[s], raw ? kNone : it);
   }
@@ -766,6 +781,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
     S.pstart[t] = 0;
     S.plen[t] = (uint16_t)(t < n_eff ? S.blen[t] - offset : 0);
     S.spsh[t] = 0;
+    S.swalk[t] = 0;
     S.szero[t] = 0;
     S.fl_head[t] = S.fl_tail[t] = kNone;
     S.cand[t] = C_NOT;
