@@ -150,3 +150,51 @@ def field_fuzz_calls(count: int = 150, seed: int = 4242):
         cap = 65535 if c % 5 else (lambda n, e=int(rng.integers(0, 3000)): OFFSET + n + e)
         calls.append((out, cap, bool(c % 6), None))
     return calls
+
+
+def long_run_calls(seed: int = 9090):
+    """[(pkts, cap, can_udp, lens_override)] long in-order TCP flows (65-128
+    packets, so a flow spans more than one 64-packet window of the kernel's
+    wave-wide append run) broken at and around the window edges: a short
+    payload, PSH, a bad checksum, a changed TOS / ack / TTL, a missing or a
+    repeated segment, the item's capacity running out, other flows
+    interleaved so a window holds non-members too."""
+    rng = np.random.default_rng(seed)
+    calls = []
+    spots = [0, 1, 31, 62, 63, 64, 65, 66, 100, 126, 127]
+    kinds = ["short", "psh", "badsum", "tos", "ack", "ttl", "gap", "dup", "none"]
+    for c in range(40):
+        v6 = bool(c % 2)
+        n = int(rng.integers(65, 129))
+        mss = int(rng.choice([200, 536, 1448]))
+        src = bytes(rng.integers(0, 256, 16 if v6 else 4, dtype=np.uint8))
+        dst = bytes(rng.integers(0, 256, 16 if v6 else 4, dtype=np.uint8))
+        seq0 = int(rng.integers(0, 2**32))
+        brk = {int(rng.choice(spots)) % n: kinds[(c + k) % len(kinds)] for k in range(int(rng.integers(1, 4)))}
+        pk, seq = [], seq0
+        for j in range(n):
+            kind = brk.get(j, "")
+            ln = int(rng.integers(1, mss)) if kind == "short" else mss
+            pay = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+            if kind == "gap":
+                seq += mss
+            if kind == "dup":
+                seq -= mss
+            p = packet(v6, False, src, dst, 5000, 51820, seq, pay, flags=0x18 if kind == "psh" else 0x10,
+                       ack=9 if kind == "ack" else 7, tos=0x10 if kind == "tos" else 0, tc=1 if kind == "tos" else 0,
+                       ttl=3 if kind == "ttl" else 64, hop=3 if kind == "ttl" else 64)
+            if kind == "badsum":
+                p = p[:-1] + bytes([p[-1] ^ 0x5A])
+            pk.append(p)
+            seq += ln
+        if c % 4 == 3:  # another flow interleaved, every third slot
+            other = _flow(rng, 128 - n if n < 128 else 0, mss, v6, False, 777 + c)
+            mixed = []
+            for j, p in enumerate(pk):
+                mixed.append(p)
+                if j % 3 == 2 and other:
+                    mixed.append(other.pop(0))
+            pk = (mixed + other)[:128]
+        cap = 65535 if c % 5 else 200000
+        calls.append((pk, cap, True, None))
+    return calls

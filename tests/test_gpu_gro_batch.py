@@ -345,3 +345,13 @@ def test_gro_batch_field_fuzz(dev):
 
     calls = gro_cases.field_fuzz_calls()
     assert _check(dev, calls) == len(calls)
+
+
+def test_gro_batch_long_runs(dev):
+    """Long in-order flows broken at and around the 64-packet window edges of
+    the kernel's wave-wide append run (tests/gro_cases.py long_run_calls), in
+    one launch, every byte against the oracle."""
+    import gro_cases
+
+    calls = gro_cases.long_run_calls()
+    assert _check(dev, calls) == len(calls)

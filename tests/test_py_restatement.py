@@ -224,15 +224,17 @@ def test_checksum_valid_short_packets_spare_capacity():
     assert seen["panic"] >= 100 and seen["invalid"] >= 100, seen
 
 
-def test_gro_field_fuzz_corpus():
+@pytest.mark.parametrize("corpus", ["field_fuzz_calls", "long_run_calls"])
+def test_gro_field_fuzz_corpus(corpus):
     """The GRO header-field fuzz calls (tests/gro_cases.py): mutated TOS, TTL,
     fragment bits, lengths, protocol, TCP flags / data offset / ack / window,
-    UDP length, truncation, trailing bytes -- both restatements agree on
-    status, toWrite, slice headers and every buffer byte."""
+    UDP length, truncation, trailing bytes; and the long in-order flows broken
+    around 64-packet boundaries -- both restatements agree on status, toWrite,
+    slice headers and every buffer byte."""
     import gro_cases
     from test_gpu_wstager import _mk
 
-    calls = gro_cases.field_fuzz_calls()
+    calls = getattr(gro_cases, corpus)()
     merged = writes = 0
     for c, (pkts, cap, can_udp, lo) in enumerate(calls):
         bc, lens = _mk(pkts, cap, gro_cases.OFFSET, lo)
@@ -244,4 +246,4 @@ def test_gro_field_fuzz_corpus():
             assert np.array_equal(bp[j], bc[j]), (c, j)
         merged += sum(1 for i in range(len(lens)) if nl_c[i] > lens[order_c[i]])
         writes += len(tw_c)
-    assert merged > 200 and writes > 500, (merged, writes)
+    assert merged > 40 and writes > 100, (merged, writes)
