@@ -11,7 +11,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 $OUT/tests.txt
 : > $OUT/ab.jsonl
 for r in 1 2; do
-  for shape in 4x32 1x128 shuffled 4x32rev; do
+  for shape in ${SHAPES:-4x32 1x128 shuffled 4x32rev}; do
     for lib in base new; do
       if [ $lib = base ]; then export WGCS_LIB=$PWD/exp/libwgcsum_base.so; else unset WGCS_LIB; fi
       steps=40; [ $shape = 4x32rev ] && steps=8

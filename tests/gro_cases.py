@@ -158,13 +158,14 @@ def long_run_calls(seed: int = 9090):
     wave-wide append run) broken at and around the window edges: a short
     payload, PSH, a bad checksum, a changed TOS / ack / TTL, a missing or a
     repeated segment, the item's capacity running out, other flows
-    interleaved so a window holds non-members too."""
+    interleaved so a window holds non-members too.  Calls 40-59: UDP flows
+    (UDP GRO walks them the same way)."""
     rng = np.random.default_rng(seed)
     calls = []
     spots = [0, 1, 31, 62, 63, 64, 65, 66, 100, 126, 127]
     kinds = ["short", "psh", "badsum", "tos", "ack", "ttl", "gap", "dup", "none"]
-    for c in range(40):
-        v6 = bool(c % 2)
+    for c in range(60):
+        v6, udp = bool(c % 2), c >= 40
         n = int(rng.integers(65, 129))
         mss = int(rng.choice([200, 536, 1448]))
         src = bytes(rng.integers(0, 256, 16 if v6 else 4, dtype=np.uint8))
@@ -180,7 +181,7 @@ def long_run_calls(seed: int = 9090):
                 seq += mss
             if kind == "dup":
                 seq -= mss
-            p = packet(v6, False, src, dst, 5000, 51820, seq, pay, flags=0x18 if kind == "psh" else 0x10,
+            p = packet(v6, udp, src, dst, 5000, 51820, seq, pay, flags=0x18 if kind == "psh" else 0x10,
                        ack=9 if kind == "ack" else 7, tos=0x10 if kind == "tos" else 0, tc=1 if kind == "tos" else 0,
                        ttl=3 if kind == "ttl" else 64, hop=3 if kind == "ttl" else 64)
             if kind == "badsum":
@@ -188,7 +189,7 @@ def long_run_calls(seed: int = 9090):
             pk.append(p)
             seq += ln
         if c % 4 == 3:  # another flow interleaved, every third slot
-            other = _flow(rng, 128 - n if n < 128 else 0, mss, v6, False, 777 + c)
+            other = _flow(rng, 128 - n if n < 128 else 0, mss, v6, udp, 777 + c)
             mixed = []
             for j, p in enumerate(pk):
                 mixed.append(p)

@@ -43,7 +43,7 @@ namespace {
 constexpr int kMaxB = WGCS_GRO_MAX_CALL;  // buffers per call (one per thread)
 constexpr int kNone = -1;
 constexpr int kVnet = 10;
-constexpr int kCoopMin = 8;  // packets of a TCP flow from which one wave walks it
+constexpr int kCoopMin = 8;  // packets of a flow from which one wave walks it
 enum : uint8_t { C_NOT = 0, C_TCP4 = 1, C_TCP6 = 2, C_UDP4 = 3, C_UDP6 = 4 };
 enum { R_NOOP = 0, R_INSERT = 1, R_COALESCED = 2 };
 enum { CC_PREPEND = -1, CC_UNAV = 0, CC_APPEND = 1 };
@@ -281,7 +281,7 @@ struct Planner {
     c.buf = S.sbuf[s];
     c.slen = S.slen[s];
     c.cap = S.bcap[S.sbuf[s]];
-    c.valid_s = S.valid[s];
+    c.valid_s = S.valid[s] && !S.it_bad[it];  // it_bad: a UDP item inserted after a bad-checksum packet (TCP: 0)
     c.stail = S.stail[s];
     c.scount = S.scount[s];
     c.ipattr = S.ipattr[c.tgt];
@@ -514,19 +514,22 @@ struct Planner {
     return result;
   }
 
-  // tcp_append_fast for a whole wave: the flow's packets from bi on, 64
-  // packet indices at a time (lane k: packet w + k, a member of the flow when
-  // its flow id is f -- a flow's packets are in index order).  Every member
-  // evaluates tcp_append_fast's checks against the item as it would be after
-  // each earlier member of the run had appended: numMerged grows by one per
-  // member, and since a member only appends when the one before it left a
-  // multiple of gsoSize without PSH, every earlier member's payload was
-  // gsoSize.  So the first member whose checks fail is exactly the packet at
-  // which the one-lane walk leaves the fast path, and every member before it
-  // appends -- all at once, each lane linking its own piece.  Returns that
-  // packet (kNone: the flow's remaining packets all appended).  c is
-  // wave-uniform.
-  __device__ int tcp_append_run(TailCache& c, int f, int bi, int n_eff, int lane) {
+  // tcp_append_fast (udp: udp_gro's append) for a whole wave: the flow's
+  // packets from bi on, 64 packet indices at a time (lane k: packet w + k, a
+  // member of the flow when its flow id is f -- a flow's packets are in index
+  // order).  Every member evaluates the append checks against the item as it
+  // would be after each earlier member of the run had appended: numMerged
+  // grows by one per member, and since a member only appends when the one
+  // before it left a multiple of gsoSize (without PSH), every earlier
+  // member's payload was gsoSize.  So the first member whose checks fail is
+  // exactly the packet at which the one-lane walk stops appending, and every
+  // member before it appends -- all at once, each lane linking its own piece.
+  // Returns that packet (kNone: the flow's remaining packets all appended).
+  // c is wave-uniform.  For UDP that packet then starts a new item, bad (in
+  // ubad) when only its own checksum kept it from appending (gro.go:1062-1075).
+  template <bool udp>
+  __device__ int append_run(TailCache& c, int f, int bi, int n_eff, int lane, int& ubad) {
+    ubad = 0;
     if (c.it == kNone) return bi;
     for (int w = bi; w < n_eff; w += 64) {  // wave-uniform
       const int q = w + lane;
@@ -546,9 +549,15 @@ struct Planner {
       const uint16_t lhs = (uint16_t)(c.g + (uint16_t)(c.g * nm));
       const bool psh = first ? c.psh != 0 : psh_prev != 0;
       const bool mult = first ? c.mult : gso_prev == c.g;
-      const bool ok = th == c.l4h && th <= 20 && R.y == c.ipattr && R.x == c.seq + (uint32_t)lhs && !psh && mult &&
-                      gso <= c.g && (int)c.cap - offset >= ((int)slen - offset) + (int)gso && (nm != 0 || c.valid_s) &&
-                      ((R.w >> 24) & 1u);
+      // TCP: tcpPacketsCanCoalesce's append branch + coalesceTCPPackets
+      // (gro.go:433-512, :709-734); UDP: udpPacketsCanCoalesce +
+      // coalesceUDPPackets (gro.go:519-544, :745-783).  Either way the
+      // appended payload is the packet's gsoSize (same IP attributes, so the
+      // same header lengths).
+      const bool l4_ok = udp || (th == c.l4h && th <= 20 && R.x == c.seq + (uint32_t)lhs && !psh);
+      const bool fits = l4_ok && R.y == c.ipattr && mult && gso <= c.g &&
+                        (int)c.cap - offset >= ((int)slen - offset) + (int)gso && (nm != 0 || c.valid_s);
+      const bool ok = fits && ((R.w >> 24) & 1u);
       const uint64_t fail = __ballot(mem && !ok);
       const uint64_t A = fail ? M & ((1ull << __builtin_ctzll(fail)) - 1ull) : M;
       if ((A >> lane) & 1ull) {
@@ -562,7 +571,7 @@ struct Planner {
       if (A) {  // the item after the run (only its last member may carry PSH or a short payload)
         const int L = 63 - __builtin_clzll(A);
         const int cnt = __builtin_popcountll(A);
-        const uint32_t gl = (uint32_t)__shfl((int)gso, L), pl = (uint32_t)__shfl((int)pshb, L);
+        const uint32_t gl = (uint32_t)__builtin_amdgcn_readlane((int)gso, L), pl = (uint32_t)__builtin_amdgcn_readlane((int)pshb, L);
         c.stail = w + L;
         c.scount += cnt;
         c.slen += (uint32_t)(cnt - 1) * c.g + gl;
@@ -577,31 +586,43 @@ struct Planner {
           c.psh = 1;
         }
       }
-      if (fail) return w + __builtin_ctzll(fail);
+      if (fail) {
+        const int F = __builtin_ctzll(fail);
+        ubad = __builtin_amdgcn_readlane((int)fits, F);
+        return w + F;
+      }
     }
     return kNone;
   }
 
-  // run_flow for a long TCP flow, by a whole wave (f wave-uniform): runs of
-  // in-order appends go through tcp_append_run; a packet that leaves it goes
-  // through tcp_gro_wave (one lane per item).
+  // run_flow for a long flow, by a whole wave (f wave-uniform): runs of
+  // in-order appends go through append_run; a packet that leaves it goes
+  // through tcp_gro_wave (one lane per item) or, for UDP (which only ever
+  // meets the flow's last item), udp_gro on lane 0.
+  template <bool udp>
   __device__ void run_flow_wave(int f, int n_eff, int lane) {
     TailCache c;
     c.it = kNone;
     c.dirty = false;
     bool try_fast = true;
+    int ubad = 0;
     for (int i = f; i != kNone;) {  // wave-uniform
       if (try_fast) {
         load_tail(c, f);
-        i = tcp_append_run(c, f, i, n_eff, lane);
+        i = append_run<udp>(c, f, i, n_eff, lane, ubad);
         if (lane == 0) flush_tail(c);  // the item loop below reads the item from LDS
         c.dirty = false;
         if (i == kNone) break;
       }
-      // in a reordered flow the in-order fast path is tried again only after
-      // the item loop appended to the flow's last item
-      const int res = tcp_gro_wave(i, f, lane);
-      try_fast = res == R_COALESCED && S.fl_tail[f] != kNone && S.stail[S.it_slot[S.fl_tail[f]]] == i;
+      int res = R_INSERT;
+      if constexpr (udp) {  // udpGRO's outcome for a packet that does not append: a new item (the flow's last)
+        if (lane == 0) insert(i, f, (uint8_t)ubad);
+      } else {
+        // in a reordered flow the in-order fast path is tried again only after
+        // the item loop appended to the flow's last item
+        res = tcp_gro_wave(i, f, lane);
+        try_fast = res == R_COALESCED && S.fl_tail[f] != kNone && S.stail[S.it_slot[S.fl_tail[f]]] == i;
+      }
       if (lane == 0) S.res[i] = (uint8_t)res;
       i = S.fnext[i];
     }
@@ -959,11 +980,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
                      (uint32_t)S.th[t] | ((uint32_t)S.iph[t] << 8) | ((uint32_t)S.psh[t] << 16) |
                          ((uint32_t)S.valid[t] << 24));
   if (live) S.rec[t] = rec;  // step 2's key-word reads ended at the barrier above
-  // a TCP flow of kCoopMin or more packets is walked by a whole wave (its
-  // in-order runs 64 packets at a time, its item loop one lane per item,
-  // run_flow_wave); the others by one thread
+  // a flow of kCoopMin or more packets is walked by a whole wave (its
+  // in-order runs 64 packets at a time, a TCP flow's item loop one lane per
+  // item, run_flow_wave); the others by one thread
   const bool leader = live && S.flow[t] == t;
-  const bool coop = leader && S.cand[t] <= C_TCP6 && S.fsize[t] >= (uint32_t)kCoopMin;
+  const bool coop = leader && S.fsize[t] >= (uint32_t)kCoopMin;
   if (coop) {
     S.coop[atomicAdd(&S.n_coop, 1)] = (int16_t)t;
     S.fbase[t] = (int16_t)atomicAdd(&S.fitem_top, (int)S.fsize[t]);  // room for one item per packet
@@ -973,7 +994,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
   const bool raw = n_eff < n;  // "invalid offset": coalescing happened, apply* did not
   Planner P{S, arena, offset};
   if (leader && !coop) P.run_flow(t);
-  for (int k = wv; k < S.n_coop; k += 4) P.run_flow_wave(S.coop[k], n_eff, lane);  // wave-uniform
+  for (int k = wv; k < S.n_coop; k += 4) {  // wave-uniform
+    const int f = S.coop[k];
+    if (S.cand[f] >= C_UDP4) P.run_flow_wave<true>(f, n_eff, lane);
+    else P.run_flow_wave<false>(f, n_eff, lane);
+  }
   __syncthreads();
 #ifdef WGCS_GRO_STAMPS
   stp[3] = __builtin_amdgcn_s_memrealtime();

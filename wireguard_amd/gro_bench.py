@@ -48,6 +48,27 @@ def flow_segments(dev, n_pkts: int, mss: int = 1448, seed: int = synth.SEED, tcp
     return out
 
 
+def udp_flow_segments(dev, n_pkts: int, mss: int = 1448, seed: int = synth.SEED):
+    """n_pkts UDP/IPv4 datagrams of ONE flow (UDP GSO super-packets of at most
+    45 segments sharing the IP/UDP header), each made by the product's GSO split."""
+    out, first = [], None
+    while len(out) < n_pkts:
+        k = min(45, n_pkts - len(out))
+        vp = bytearray(synth.make_super_packet(28 + k * mss, mss, seed=seed + 7919 * len(out), udp=True))
+        if first is None:
+            first = bytes(vp[10:38])
+        else:  # the flow's header, lengths for this super-packet
+            vp[10:38] = first
+            vp[12:14] = (28 + k * mss).to_bytes(2, "big")
+            vp[34:36] = (8 + k * mss).to_bytes(2, "big")
+        bufs = [np.zeros(mss + 200, np.uint8) for _ in range(k + 2)]
+        sizes = [0] * len(bufs)
+        n, err = dev.handle_virtio_read(np.frombuffer(vp, np.uint8).copy(), bufs, sizes, OFFSET)
+        assert err is None and n == k, (n, err)
+        out += [bufs[i][OFFSET: OFFSET + sizes[i]].tobytes() for i in range(n)]
+    return out
+
+
 def make_batch(dev, flows: int = 4, per_flow: int = 32, mss: int = 1448, seed: int = synth.SEED):
     """128 segmented TCP/IPv4 packets, produced by the product's GSO split of
     one super-packet per flow (flows interleaved round-robin, in order per flow)."""
@@ -63,6 +84,8 @@ CALL_SHAPES = {
     "4x32rev": "4 flows x 32 segments, each flow in reverse order: every packet prepends to its item (gro.go:648-697)",
     "1x128rev": "one flow of 128 segments in reverse order (a 128-step prepend chain)",
     "shuffled": "4 flows x 32 segments in a seeded random order (appends, prepends and new items mixed)",
+    "4x32udp": "4 UDP/IPv4 flows x 32 1448-B datagrams, interleaved (UDP GRO: every datagram appends)",
+    "1x128udp": "one UDP/IPv4 flow of 128 1448-B datagrams",
 }
 
 
@@ -75,6 +98,11 @@ def shape_batch(dev, shape: str):
     if shape == "4x32rev":
         segs = [flow_segments(dev, 32, seed=synth.SEED + f)[::-1] for f in range(4)]
         return [segs[f][k] for k in range(32) for f in range(4)]
+    if shape == "4x32udp":
+        segs = [udp_flow_segments(dev, 32, seed=synth.SEED + f) for f in range(4)]
+        return [segs[f][k] for k in range(32) for f in range(4)]
+    if shape == "1x128udp":
+        return udp_flow_segments(dev, 128)
     if shape == "shuffled":
         pk = make_batch(dev)
         order = np.random.default_rng(synth.SEED).permutation(len(pk))
