@@ -69,7 +69,7 @@ def parse():
                     help="gro_staged: host threads pushing Write calls concurrently (default 4)")
     ap.add_argument("--pinned", action="store_true",
                     help="gro_staged: Write buffers in pinned host memory, zero-copy pushes")
-    ap.add_argument("--gro-shape", default="4x32", choices=["4x32", "1x128", "4x32rev", "1x128rev", "shuffled", "4x32udp", "1x128udp"],
+    ap.add_argument("--gro-shape", default="4x32", choices=["4x32", "1x128", "4x32rev", "1x128rev", "shuffled", "4x32udp", "1x128udp", "16x8", "32x4"],
                     help="gro_device: the packets of each Write call (wireguard_amd/gro_bench.py CALL_SHAPES)")
     ap.add_argument("--max-segs", type=int, default=128,
                     help="cfg4: output slots per read = len(bufs) (the reference's Read passes conn.BatchSize = 128)")

@@ -12,8 +12,8 @@ tail -2 $OUT/tests.txt
 : > $OUT/ab.jsonl
 for r in 1 2; do
   for shape in ${SHAPES:-4x32 1x128 shuffled 4x32rev}; do
-    for lib in base new; do
-      if [ $lib = base ]; then export WGCS_LIB=$PWD/exp/libwgcsum_base.so; else unset WGCS_LIB; fi
+    for lib in ${LIBS:-base new}; do
+      if [ $lib = new ]; then unset WGCS_LIB; else export WGCS_LIB=$PWD/exp/libwgcsum_$lib.so; fi
       steps=40; [ $shape = 4x32rev ] && steps=8
       timeout -k 10 150 python bench.py --config gro_device --gro-shape $shape --steps $steps --warmup 3 --cpu-seconds 0 --no-e2e > $OUT/run.log 2>&1 || { echo "rc=$? $shape $lib"; tail -5 $OUT/run.log; exit 1; }
       grep '^{' $OUT/run.log | sed "s/^{/{\"lib\": \"$lib\", \"shape\": \"$shape\", \"round\": $r, /" >> $OUT/ab.jsonl

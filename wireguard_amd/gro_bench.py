@@ -86,6 +86,8 @@ CALL_SHAPES = {
     "shuffled": "4 flows x 32 segments in a seeded random order (appends, prepends and new items mixed)",
     "4x32udp": "4 UDP/IPv4 flows x 32 1448-B datagrams, interleaved (UDP GRO: every datagram appends)",
     "1x128udp": "one UDP/IPv4 flow of 128 1448-B datagrams",
+    "16x8": "16 TCP/IPv4 flows x 8 in-order segments, interleaved (many short flows)",
+    "32x4": "32 TCP/IPv4 flows x 4 in-order segments, interleaved",
 }
 
 
@@ -98,6 +100,9 @@ def shape_batch(dev, shape: str):
     if shape == "4x32rev":
         segs = [flow_segments(dev, 32, seed=synth.SEED + f)[::-1] for f in range(4)]
         return [segs[f][k] for k in range(32) for f in range(4)]
+    if shape in ("16x8", "32x4"):
+        f, k = (int(x) for x in shape.split("x"))
+        return make_batch(dev, flows=f, per_flow=k)
     if shape == "4x32udp":
         segs = [udp_flow_segments(dev, 32, seed=synth.SEED + f) for f in range(4)]
         return [segs[f][k] for k in range(32) for f in range(4)]
