@@ -11,7 +11,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-SO = os.path.join(ROOT, "scripts", "probe_so", "libwgcsum_grostamps.so")
+SO = os.environ.get("WGCS_STAMPS_SO") or os.path.join(ROOT, "scripts", "probe_so", "libwgcsum_grostamps.so")
 
 if len(sys.argv) > 1 and sys.argv[1] == "build":
     from wireguard_amd import build as B

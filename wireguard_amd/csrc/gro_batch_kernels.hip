@@ -43,7 +43,7 @@ namespace {
 constexpr int kMaxB = WGCS_GRO_MAX_CALL;  // buffers per call (one per thread)
 constexpr int kNone = -1;
 constexpr int kVnet = 10;
-constexpr int kCoopMin = 8;  // packets of a flow from which one wave walks it
+constexpr int kCoopMin = 16;  // packets of a flow from which one wave walks it (r4_gro_walk: 16x8 walks 22 -> 4 us)
 enum : uint8_t { C_NOT = 0, C_TCP4 = 1, C_TCP6 = 2, C_UDP4 = 3, C_UDP6 = 4 };
 enum { R_NOOP = 0, R_INSERT = 1, R_COALESCED = 2 };
 enum { CC_PREPEND = -1, CC_UNAV = 0, CC_APPEND = 1 };
