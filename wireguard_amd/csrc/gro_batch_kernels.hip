@@ -465,20 +465,39 @@ struct Planner {
     {  // nit <= 64: one lane per item
       const int k = lane;
       int code = W_SKIP, can = CC_UNAV, it = kNone;
+      const uint4 R = S.rec[bi];  // the packet: {seq, ipattr, gsoSize, th | iph | PSH | valid}
+      const uint32_t pth = R.w & 0xFFu;
       if (k < nit) {
+        // tcp_can and coalesceTCPPackets' checks without early exits, so
+        // each lane issues its item's LDS reads together (three dependent
+        // levels: item, slot, head packet / buffer), not one round trip per check
         it = S.fitem[base + nit - 1 - k];
-        can = tcp_can(bi, it);
-        if (can != CC_UNAV) {
-          const int s = S.it_slot[it];
-          const int pl = plen_slot(bi);
-          const int hdrs = (uint8_t)(S.it_iph[it] + S.it_l4h[it]);
-          const int new_len = plen_slot(s) + pl - hdrs;
-          const int cap = (int)S.bcap[can == CC_PREPEND ? S.sbuf[bi] : S.sbuf[s]] - offset;
-          if (cap < new_len || (can == CC_PREPEND && S.psh[bi])) code = W_SKIP;  // coalesceInsufficientCap / PSHEnding
-          else if (S.it_nm[it] == 0 && !S.valid[s]) code = W_DEL;                  // coalesceItemInvalidChecksum
-          else if (!S.valid[bi]) code = W_STOP;                                    // coalescePktInvalidChecksum
-          else code = W_OK;
-        }
+        const int s = S.it_slot[it];
+        const uint32_t l4h = S.it_l4h[it], g = S.it_gso[it], nm = S.it_nm[it], iseq = S.it_seq[it];
+        const bool ipsh = S.it_psh[it] != 0;
+        const int hdrs = (uint8_t)(S.it_iph[it] + l4h);
+        const int tgt = S.shead[s];
+        const int plen_s = plen_slot(s);
+        const bool vs = S.valid[s] != 0;
+        const uint32_t tattr = S.ipattr[tgt];
+        const int cap_s = (int)S.bcap[S.sbuf[s]] - offset;
+        const int pl_b = plen_slot(bi), cap_b = (int)S.bcap[S.sbuf[bi]] - offset;  // the packet's own slot
+        const uint32_t pseq = R.x, pgso = R.z & 0xFFFFu, piph = (R.w >> 8) & 0xFFu;
+        const bool ppsh = (R.w >> 16) & 1u, pvalid = (R.w >> 24) & 1u;
+        // tcpPacketsCanCoalesce (gro.go:433-512), as tcp_can
+        const uint16_t lhs = (uint16_t)(g + (uint16_t)(g * nm));
+        const bool app = pseq == iseq + (uint32_t)lhs;
+        const bool app_ok = !ipsh && (plen_s - (int)(piph + pth)) % (int)g == 0 && pgso <= g;
+        const bool pre_ok = pseq + pgso == iseq && !ppsh && pgso >= g && !(pgso > g && nm > 0);
+        can = (pth != l4h || R.y != tattr) ? CC_UNAV : app ? (app_ok ? CC_APPEND : CC_UNAV) : pre_ok ? CC_PREPEND : CC_UNAV;
+        if (pth > 20 && can != CC_UNAV && !options_equal(bi, tgt, S.it_iph[it])) can = CC_UNAV;  // TCP options (gro.go:442-448)
+        const int new_len = plen_s + pl_b - hdrs;
+        const int cap = can == CC_PREPEND ? cap_b : cap_s;
+        code = can == CC_UNAV                                       ? W_SKIP
+               : (cap < new_len || (can == CC_PREPEND && ppsh))     ? W_SKIP   // coalesceInsufficientCap / PSHEnding
+               : (nm == 0 && !vs)                                   ? W_DEL    // coalesceItemInvalidChecksum
+               : !pvalid                                            ? W_STOP   // coalescePktInvalidChecksum
+                                                                    : W_OK;
       }
       const uint64_t dec = __ballot(code >= W_STOP);
       const uint64_t del = __ballot(code == W_DEL) & (dec ? ((1ull << __builtin_ctzll(dec)) - 1ull) : ~0ull);
