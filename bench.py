@@ -84,6 +84,8 @@ def parse():
                     help="cfg2: skip the configs[4] block (the 1M mixed batch split over the ranks, `cfg5_strong`)")
     ap.add_argument("--no-gate", action="store_true",
                     help="enqueue the K steps inside the timed region instead of posting them behind a doorbell")
+    ap.add_argument("--poll", action="store_true",
+                    help="poll the closing event before torch.cuda.synchronize() (slower: profiles/r4_probe_poll_ab.jsonl)")
     ap.add_argument("--no-affinity", action="store_true", help="do not bind each rank to its GPU's NUMA-local CPUs")
     ap.add_argument("--repeat", type=int, default=1,
                     help="diagnostics: time the K-step region this many times; `value` stays the FIRST region, "
@@ -216,7 +218,8 @@ def main():
     bytes_per_step = int(pkts_np["len"].astype(np.int64).sum())
     use_events = not args.no_event_timing
     leg = checksum_leg(torch, dev, arena_np, pkts_np, mode, args.steps, args.warmup, args.streams, args.rotate,
-                       barrier, use_events, repeat=args.repeat, verify=args.verify, gate=not args.no_gate)
+                       barrier, use_events, repeat=args.repeat, verify=args.verify, gate=not args.no_gate,
+                       poll=args.poll)
     local_elapsed, kern_ms, iso_ms, S, R = leg["elapsed"], leg["kern_ms"], leg["iso_ms"], leg["streams"], leg["R"]
     elapsed = shard.max_over_ranks(local_elapsed, dist, device=red_dev)
     kern_all = shard.gather_floats(kern_ms if kern_ms is not None else -1.0, dist, device=red_dev)
@@ -268,7 +271,9 @@ def main():
                             "wall_minus_span_us": round((local_elapsed - kern_ms * args.steps * 1e-3) * 1e6, 2),
                             "enqueue": ("one wgcs_checksum_batches call for the K steps" +
                                         ("" if args.no_gate else ", posted behind a doorbell (wgcs_stream_wait_flag) "
-                                         "rung when the clock starts"))}
+                                         "rung when the clock starts") +
+                                        ("; completion polled on the closing event, then torch.cuda.synchronize()"
+                                         if args.poll else ""))}
         if leg["repeats"]:
             result["timing"]["repeats"] = [{"wall_us": round(w * 1e6, 1), "event_span_us": round(m * args.steps * 1e3, 1)}
                                            for w, m in leg["repeats"]]
@@ -381,7 +386,7 @@ def roofline(kname, bytes_per_step, flen, n, kern_ms, S, iso_ms, kern_all=None) 
 
 
 def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, rotate, barrier, use_events,
-                 repeat=1, verify=False, iso=True, gate=True):
+                 repeat=1, verify=False, iso=True, gate=True, poll=False):
     """Time `steps` checksum launches (one batch each, inputs resident in HBM)
     after `warmup` untimed ones.  Returns {elapsed (this rank's wall s),
     kern_ms (HIP events, GPU ms per launch), iso_ms (one-stream reference),
@@ -442,6 +447,12 @@ def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, ro
         else:
             t0 = time.perf_counter()
             dev.checksum_batches(mode, bl, strm[:ns], *evs)
+        # Completion: torch.cuda.synchronize().  Polling the closing event
+        # first (--poll) was measured slower: 30-35 us of wall time beyond the
+        # GPU's event span against 11-12 us (profiles/r4_probe_poll_ab.jsonl).
+        if poll and use_events:
+            while not e1.query():
+                pass
         torch.cuda.synchronize()
         el = time.perf_counter() - t0  # the closing barrier is not timed: max over ranks covers skew
         barrier()
@@ -497,7 +508,7 @@ def strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_
     bytes_rank = int(pkts_np["len"].astype(np.int64).sum())
     S = 2
     leg = checksum_leg(torch, dev, arena_np, pkts_np, mode, args.steps, args.warmup, S, 2, barrier, use_events,
-                       iso=False, gate=not args.no_gate)
+                       iso=False, gate=not args.no_gate, poll=args.poll)
     del arena_np
     elapsed = shard.max_over_ranks(leg["elapsed"], dist, device=red_dev)
     kern_all = shard.gather_floats(leg["kern_ms"] if leg["kern_ms"] is not None else -1.0, dist, device=red_dev)
