@@ -428,7 +428,10 @@ struct Planner {
   // loop goes on past them); no such item: the packet is inserted.  Then lane 0
   // applies the outcome.  Returns the groResult.
   enum { W_SKIP = 0, W_DEL = 1, W_STOP = 2, W_OK = 3 };
-  __device__ int tcp_gro_wave(int bi, int f, int lane) {
+  // tail_app: 1 when bi appended to the flow's last item, 0 when not, -1 when
+  // not known here (the one-lane loop)
+  __device__ int tcp_gro_wave(int bi, int f, int lane, int& tail_app) {
+    tail_app = -1;
     const int base = S.fbase[f];
     int nit = S.fnit[f];
     int result = R_INSERT, mode = CC_UNAV, it_ok = kNone;
@@ -516,6 +519,10 @@ struct Planner {
         mode = __shfl(can, d);
         it_ok = __shfl(it, d);
         result = cd == W_OK ? R_COALESCED : R_NOOP;
+        // the items after it (lanes below d) are all deleted: it is the last one now
+        tail_app = result == R_COALESCED && mode == CC_APPEND && d == (int)__builtin_popcountll(del);
+      } else {
+        tail_app = 0;
       }
       nit -= (int)__builtin_popcountll(del);
     }
@@ -639,8 +646,10 @@ struct Planner {
       } else {
         // in a reordered flow the in-order fast path is tried again only after
         // the item loop appended to the flow's last item
-        res = tcp_gro_wave(i, f, lane);
-        try_fast = res == R_COALESCED && S.fl_tail[f] != kNone && S.stail[S.it_slot[S.fl_tail[f]]] == i;
+        int tail_app;
+        res = tcp_gro_wave(i, f, lane, tail_app);
+        try_fast = tail_app >= 0 ? tail_app != 0
+                                 : res == R_COALESCED && S.fl_tail[f] != kNone && S.stail[S.it_slot[S.fl_tail[f]]] == i;
       }
       if (lane == 0) S.res[i] = (uint8_t)res;
       i = S.fnext[i];
