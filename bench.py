@@ -274,6 +274,14 @@ def main():
                                          "rung when the clock starts") +
                                         ("; completion polled on the closing event, then torch.cuda.synchronize()"
                                          if args.poll else ""))}
+        if leg.get("ungated"):
+            uw, um = leg["ungated"]
+            result["timing"]["ungated"] = {
+                "what": "the same K steps enqueued inside the clock (no doorbell), timed after the region; "
+                        "how rounds 1-3 timed; never `value`",
+                "wall_us": round(uw * 1e6, 2), "GiB_per_s": round(bytes_per_step * args.steps / uw / 2**30, 2)}
+            if um is not None:
+                result["timing"]["ungated"]["event_span_us"] = round(um * args.steps * 1e3, 2)
         if leg["repeats"]:
             result["timing"]["repeats"] = [{"wall_us": round(w * 1e6, 1), "event_span_us": round(m * args.steps * 1e3, 1)}
                                            for w, m in leg["repeats"]]
@@ -431,14 +439,18 @@ def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, ro
     # launches' GPU work and the completion wait, not the host's enqueue calls.
     bell = dev.host_alloc(64).view(np.uint32) if gate else None
 
-    def timed(K, k0, ns):
+    def timed(K, k0, ns, gated=True):
         bl = batches(K, k0)  # the step list (pointers only) is built before the clock starts
         barrier()
         torch.cuda.synchronize()
         evs = (e0 if use_events else None, e1 if use_events else None)
-        if bell is not None:
+        if bell is not None and gated:
             bell[0] = 0
-            dev.stream_wait_flag(strm[0], bell, 1)  # streams[1:] wait on e0, recorded behind it
+            # every launch stream waits on the bell itself: streams[1:] also
+            # wait on e0 when the events are on, but without events nothing
+            # else would hold them before the clock starts
+            for s in strm[:ns]:
+                dev.stream_wait_flag(s, bell, 1)
             try:
                 dev.checksum_batches(mode, bl, strm[:ns], *evs)
             finally:
@@ -487,10 +499,17 @@ def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, ro
 
     local_elapsed, kern_ms = timed(steps, warmup, S)
     repeats = [timed(steps, warmup + r * steps, S) for r in range(1, repeat)]
+    # The same K steps enqueued inside the clock (no doorbell), after the
+    # timed region: the rounds before round 4 timed this way, so the line
+    # carries both wall times for comparison (never `value`)
+    ungated = None
+    if bell is not None and iso:
+        ungated = timed(steps, warmup + repeat * steps, S, gated=False)
     if iso and use_events and S > 1 and not iso_first:  # the same launches one at a time on one stream
         _, iso_ms = timed(max(steps, 20), warmup + steps, 1)
     del arenas, outs, pkts
-    return {"elapsed": local_elapsed, "kern_ms": kern_ms, "iso_ms": iso_ms, "repeats": repeats, "streams": S, "R": R}
+    return {"elapsed": local_elapsed, "kern_ms": kern_ms, "iso_ms": iso_ms, "repeats": repeats, "streams": S, "R": R,
+            "ungated": ungated}
 
 
 def strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_events) -> dict:

@@ -202,6 +202,42 @@ int main(void) {
   }
   for (int i = 0; i < n_p; ++i) CHECK(memcmp(bp[i], bo[i], CAP) == 0, "GRO buffer %d differs", i);
 
+  /* ---- handleGRO with a zero-capacity buffer after two segments: the cgo
+   * shim passes a NULL pointer with len = cap = 0 for it,
+   * the reference returns "invalid offset" at that buffer (gro.go:1334-1337)
+   * after the earlier ones went through tcpGRO, and apply* never runs ---- */
+  {
+    uint8_t *zp[3], *zo[3];
+    size_t zl_p[3], zc_p[3], zl_o[3], zc_o[3];
+    for (int i = 0; i < 2; ++i) {
+      zp[i] = malloc(CAP);
+      zo[i] = malloc(CAP);
+      memcpy(zp[i], seg[i], CAP);
+      memcpy(zo[i], seg[i], CAP);
+      zl_p[i] = zl_o[i] = (size_t)(OFFSET + sz_o[i]);
+      zc_p[i] = zc_o[i] = CAP;
+    }
+    zp[2] = zo[2] = NULL;
+    zl_p[2] = zl_o[2] = zc_p[2] = zc_o[2] = 0;
+    int ztw_p[3], ztw_o[3], zn_p = -1, zn_o = -1;
+    rc = wgcs_handle_gro(ctx, zp, zl_p, zc_p, 3, OFFSET, 1, ztw_p, &zn_p);
+    const int zrc = or_handle_gro(zo, zl_o, zc_o, 3, OFFSET, 1, ztw_o, &zn_o);
+    CHECK(rc == WGCS_ERR_INVALID_OFFSET && zrc == OR_ERR_INVALID_OFFSET,
+          "zero-capacity buffer: rc %d / %d, want invalid offset", rc, zrc);
+    CHECK(zn_p == zn_o, "zero-capacity buffer: writes %d / %d", zn_p, zn_o);
+    for (int k = 0; k < zn_p; ++k) CHECK(ztw_p[k] == ztw_o[k], "zero-capacity buffer: toWrite[%d]", k);
+    CHECK(zp[2] == NULL && zl_p[2] == 0 && zc_p[2] == 0, "zero-capacity buffer: its slice header changed");
+    CHECK(zo[2] == NULL && zl_o[2] == 0 && zc_o[2] == 0, "zero-capacity buffer: oracle slice header changed");
+    for (int i = 0; i < 2; ++i) {
+      CHECK(zl_p[i] == zl_o[i] && zc_p[i] == zc_o[i], "zero-capacity call: slice %d len/cap", i);
+      CHECK(memcmp(zp[i], zo[i], CAP) == 0, "zero-capacity call: buffer %d differs", i);
+    }
+    for (int i = 0; i < 2; ++i) {
+      free(zp[i]);
+      free(zo[i]);
+    }
+  }
+
   /* ---- conn: splitMessages on a recvmmsg batch (2 UDP_GRO datagrams) ---- */
   {
     enum { NM = 128, FIRST = 126, BL = 65535, SEG = 1452, NSEG = 45 };

@@ -207,3 +207,41 @@ def test_stream_wait_flag_doorbell(dev):
     want = oracle.checksum_batch(MODE_VALIDATE, arena, pkts)
     assert np.array_equal(d_out.cpu().numpy(), want) and want.all()
     dev.host_free(bell.view(np.uint8))
+
+
+def test_doorbell_gates_every_stream_without_events(dev):
+    """bench.py's gate with --no-event-timing and two launch streams: every
+    launch stream waits on the doorbell itself, so no batch of the series runs
+    before the ring even with no bracket events joining the streams (ADVICE
+    r4: only stream 0 used to be gated)."""
+    import time
+
+    import torch
+
+    import oracle
+    from wireguard_amd import synth
+    from wireguard_amd.tun import MODE_VALIDATE
+
+    arena, pkts, _ = synth.make_batch(512, 1500, kinds="mixed")
+    d_arena = torch.from_numpy(arena).cuda()
+    d_pkts = torch.from_numpy(pkts.view(np.uint8)).cuda()
+    outs = [torch.full((512,), 7, dtype=torch.uint8, device="cuda") for _ in range(4)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    bell = dev.host_alloc(64).view(np.uint32)
+    torch.cuda.synchronize()
+    bell[0] = 0
+    for s in streams:
+        dev.stream_wait_flag(s, bell, 1)
+    dev.checksum_batches(MODE_VALIDATE, dev.batch_list([(d_arena, d_pkts, 512, o) for o in outs]), streams)
+    evs = [torch.cuda.Event() for _ in streams]
+    for e, s in zip(evs, streams):
+        e.record(s)
+    time.sleep(0.05)
+    ran = [e.query() for e in evs]
+    bell[0] = 1  # ring before any assert: never leave a stream gated
+    torch.cuda.synchronize()
+    assert not any(ran), f"a stream ran before the doorbell: {ran}"
+    want = oracle.checksum_batch(MODE_VALIDATE, arena, pkts)
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy(), want)
+    dev.host_free(bell.view(np.uint8))

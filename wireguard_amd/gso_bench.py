@@ -44,8 +44,11 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
     R = max(R, 2 * S)
     d_arena = [torch.from_numpy(arena).cuda() for _ in range(R)]
     d_jobs = torch.from_numpy(jobs.view(np.uint8)).cuda()
-    d_out = [torch.empty(n_jobs * max_segs * stride + 256, dtype=torch.uint8, device="cuda")[oshift:]
+    # slack past the slots covers the base shift (< out_align) as well as 256 B
+    # (a fixed 256 B let an --gso-out-align above 256 cut the view short)
+    d_out = [torch.empty(n_jobs * max_segs * stride + max(out_align, 256), dtype=torch.uint8, device="cuda")[oshift:]
              for _ in range(R)]
+    assert all(d.numel() >= n_jobs * max_segs * stride for d in d_out)
     # per-stream result arrays: launches on different streams may overlap
     d_sizes = [torch.zeros(n_jobs * max_segs, dtype=torch.int32, device="cuda") for _ in range(S)]
     d_count = [torch.zeros(n_jobs, dtype=torch.int32, device="cuda") for _ in range(S)]
