@@ -7,6 +7,9 @@ of its job (max_segs 128, 45 segments per job):
   T0 wave start, T1 verdict + job sums done (the payload loads issue next),
   T2 payload stream done (loads consumed, stores issued), T3 header stored,
   T4 after s_waitcnt vmcnt(0) (the wave's stores acknowledged).
+gso_lds_kernel (NWAVES=<its waves per job>): T0 start, T1 verdict + job sums,
+T2 the LDS image landed (after vmcnt(0) + barrier), T3 every row's segments
+streamed and stored, T4 stores acknowledged.
 With -DWGCS_GSO_STAMPS=2 (run with STAMPS=2) the head of the wave instead:
   T0 start, T1 job descriptor arrived, T2 virtio header + header chunks
   arrived, T3 verdict + job sums done, T4 payload stream done.
@@ -42,14 +45,21 @@ dev = Device(0)
 n_jobs, total, gso, max_segs, stride, offset = 256, 65535, 1460, 128, 1536, 16
 pkts = [synth.make_super_packet(total, gso, seed=synth.SEED + k) for k in range(n_jobs)]
 jlen = len(pkts[0])
-arena = np.frombuffer(b"".join(pkts) + bytes(64), dtype=np.uint8).copy()
+# ALIGN=128 (default): bench.py cfg4's layout -- each read at a 128-B multiple
+# of the arena, bufs[i][offset] on a 128-B line; ALIGN=0: packed, as allocated
+ALIGN = int(os.environ.get("ALIGN", "128"))
+jpitch = -(-jlen // ALIGN) * ALIGN if ALIGN else jlen
+arena = np.zeros(n_jobs * jpitch + 64, np.uint8)
+for k, p in enumerate(pkts):
+    arena[k * jpitch: k * jpitch + jlen] = np.frombuffer(p, np.uint8)
 jobs = np.zeros(n_jobs, GSO_JOB_DTYPE)
-jobs["off"] = np.arange(n_jobs, dtype=np.uint64) * np.uint64(jlen)
+jobs["off"] = np.arange(n_jobs, dtype=np.uint64) * np.uint64(jpitch)
 jobs["len"] = jlen
+oshift = (ALIGN - offset % ALIGN) % ALIGN if ALIGN else 0
 R = int(os.environ.get("PROBE_R", "8"))  # rotated arena / output copies
 d_arena = [torch.from_numpy(arena).cuda() for _ in range(R)]
 d_jobs = torch.from_numpy(jobs.view(np.uint8)).cuda()
-d_out = [torch.empty(n_jobs * max_segs * stride, dtype=torch.uint8, device="cuda") for _ in range(R)]
+d_out = [torch.empty(n_jobs * max_segs * stride + 256, dtype=torch.uint8, device="cuda")[oshift:] for _ in range(R)]
 streams = [torch.cuda.Stream(), torch.cuda.Stream()]
 d_sizes = [torch.zeros(n_jobs * max_segs, dtype=torch.int32, device="cuda") for _ in range(2)]
 d_count = [torch.zeros(n_jobs, dtype=torch.int32, device="cuda") for _ in range(2)]
@@ -79,8 +89,12 @@ def run(K, ns, k0):
     return e0.elapsed_time(e1) * 1e3 / K
 
 
+NWAVES = int(os.environ.get("NWAVES", "12"))  # stamp-writing waves per job: 12 (rows kernel), NW (gso_lds_kernel)
+
+
 def stamps(q):
-    s = d_sizes[q].cpu().numpy().reshape(n_jobs, max_segs)[:, 64:124].reshape(n_jobs, 12, 5).astype(np.int64)
+    s = d_sizes[q].cpu().numpy().reshape(n_jobs, max_segs)[:, 64:64 + 5 * NWAVES].reshape(n_jobs, NWAVES, 5)
+    s = s.astype(np.int64)
     return s.reshape(-1, 5) & 0xFFFFFFFF
 
 
@@ -88,7 +102,8 @@ def summary(st, base):
     us = (st - base) * 0.01  # 100 MHz ticks -> us
     out = {}
     names = (["T0_start", "T1_desc", "T2_hdr_loads", "T3_sums", "T4_stream_done"] if os.environ.get("STAMPS") == "2"
-             else ["T0_start", "T1_verdict", "T2_stream_done", "T3_hdr_done", "T4_stores_acked"])
+             else ["T0_start", "T1_verdict", "T2_image_landed", "T3_rows_done", "T4_stores_acked"]
+             if os.environ.get("NWAVES") else ["T0_start", "T1_verdict", "T2_stream_done", "T3_hdr_done", "T4_stores_acked"])
     for k, name in enumerate(names):
         v = us[:, k]
         out[name] = [round(float(np.percentile(v, p)), 2) for p in (0, 10, 50, 90, 100)]

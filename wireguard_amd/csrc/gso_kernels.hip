@@ -635,6 +635,80 @@ __device__ __forceinline__ void consume_batch(const uint4 (&A)[U], uint32_t E, i
   }
 }
 
+#ifndef WGCS_GSO_WT
+#define WGCS_GSO_WT 1  // write-through full-chunk stores in gso_lds_kernel (0: plain stores, A/B builds)
+#endif
+#ifndef WGCS_GSO_WT_AUX
+#define WGCS_GSO_WT_AUX 16  // the write-through stores' cache policy: 16 = sc1 (A/B builds: 0 plain, 2 nt, 17 sc0 sc1)
+#endif
+// Where gso_lds_kernel's row writes: its segment's destination chunks at
+// dbase (= out + obase + dro), and, when `wt`, a buffer resource over the
+// job's output region (out + obase) for write-through full-chunk stores
+// (`sc1`: the line leaves L2 at once instead of staying dirty until the
+// end-of-kernel writeback).  The stores go through the buffer intrinsic, not
+// inline asm: the compiler then sees them (wait counts, and the hazard of a
+// VALU overwriting a 16-byte store's data registers right behind it).
+struct RowOut {
+  uint4 keep;  // this lane's header-shared chunk's payload bytes (consume_batch_img)
+  __amdgpu_buffer_rsrc_t rs;
+  int dro;  // dbase - (out + obase), when wt
+  bool wt;  // block-uniform: every offset of the job's output region fits the resource
+};
+__device__ __forceinline__ void store16_row(const RowOut& o, uint8_t* dbase, int ko, const uint4& v) {
+  if (o.wt) {
+    typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+    const u32x4v vv = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(vv, o.rs, o.dro + ko, 0, WGCS_GSO_WT_AUX);
+  } else {
+    *reinterpret_cast<uint4*>(dbase + ko) = v;
+  }
+}
+// store_chunk with its full-chunk case through store16_row.
+__device__ __forceinline__ void store_chunk_row(const RowOut& o, uint8_t* dbase, int ko, const uint4& v, int x0,
+                                                int pkt_len) {
+  if (x0 >= 0 && x0 + 16 <= pkt_len) store16_row(o, dbase, ko, v);
+  else store_chunk(dbase + ko, v, x0, pkt_len);
+}
+
+// consume_batch for gso_lds_kernel.  A chunk the row shares with the header
+// (x0 < hdrLen: only step 0 of the first batch, hdrLen + dalign <= 255) is not
+// stored here: its payload bytes are kept in `keep` (lane r: chunk r) and
+// finish_row stores them with the header bytes as one 16-byte store.  Whole
+// payload chunks are stored write-through, the packet's last partial chunk as
+// pieces.  The sums are consume_batch's.
+template <int U>
+__device__ __forceinline__ void consume_batch_img(const uint4 (&A)[U], uint32_t E, int k0, const RowSrc& g,
+                                                  int hdr_len, int dalign, uint8_t* dbase, int r, uint32_t& acc,
+                                                  RowOut& ro) {
+  const int pkt_len = g.pkt_len, sb = g.sb;
+  uint32_t Rc = row_next(A[0].x);  // lane 15: lane 0's next-u dword
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int k = k0 + r + 16 * u;
+    const uint32_t Rx = u + 1 < U ? row_next(A[u + 1 < U ? u + 1 : u].x) : E;
+    const uint32_t nx = r == 15 ? Rx : Rc;
+    Rc = Rx;
+    const int x0 = 16 * k - dalign;
+    const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(A[u].y, A[u].x, sb),
+                               __builtin_amdgcn_alignbyte(A[u].z, A[u].y, sb),
+                               __builtin_amdgcn_alignbyte(A[u].w, A[u].z, sb),
+                               __builtin_amdgcn_alignbyte(nx, A[u].w, sb));
+    int ko = 16 * k;
+    asm volatile("" : "+v"(ko));
+    if (wave_none(x0 < hdr_len || x0 + 16 > pkt_len)) {  // every chunk of the step whole payload
+      acc = add4(acc, v);
+      store16_row(ro, dbase, ko, v);
+    } else {
+      acc = add4_masked(acc, v, byte_bits16(hdr_len - x0, pkt_len - x0), false);
+      if (u == 0) ro.keep = k0 == 0 ? v : ro.keep;
+      if (x0 >= hdr_len && x0 < pkt_len) {
+        if (x0 + 16 <= pkt_len) store16_row(ro, dbase, ko, v);
+        else store_lo(dbase + ko, v, pkt_len - x0);  // the packet's last bytes
+      }
+    }
+  }
+}
+
 // One row's whole payload stream, batch by batch.
 template <int U, bool NT>
 __device__ __forceinline__ void stream_row(const uint8_t* rb, int i, int gso, int hdr_len, int plen, int dalign,
@@ -741,7 +815,8 @@ __device__ __noinline__ void decode_publish(const uint8_t* vb, uint32_t jlen, ui
 __device__ __forceinline__ void finish_row(bool fast, const uint4 Q, int type, int ipv, int hdr_len, int gso, int cs,
                                            int co, int plen, int i, int r, int dalign, const uint8_t* dst,
                                            uint8_t* dbase, uint32_t acc, uint32_t ip_base, uint32_t l4_base,
-                                           uint32_t tflags, uint32_t id0, uint32_t seq0, int32_t* size_out) {
+                                           uint32_t tflags, uint32_t id0, uint32_t seq0, int32_t* size_out,
+                                           const RowOut* ro = nullptr) {
   const uint4 z = make_uint4(0, 0, 0, 0);
   // ---- segment geometry (row-uniform)
   const bool v4 = ipv == 4, tcp = type != GSO_UDP_L4;
@@ -788,7 +863,14 @@ __device__ __forceinline__ void finish_row(bool fast, const uint4 Q, int type, i
     // merged with the payload bytes, stored
     const uint4 Pp = row_prev4(P);
     const uint4 D = dalign ? funnel_v(Pp, P, 16 - dalign) : P;
-    if (r < hk) store_chunk(dbase + 16 * r, D, x0h, hdr_len);  // header bytes [0, hdrLen)
+    if (ro) {
+      // gso_lds_kernel: the stream kept these chunks' payload bytes
+      // (consume_batch_img); header and payload go out as one store
+      if (r < hk)
+        store_chunk_row(*ro, dbase, 16 * r, select_bytes(D, ro->keep, byte_bits16(-x0h, hdr_len - x0h)), x0h, pkt_len);
+    } else if (r < hk) {
+      store_chunk(dbase + 16 * r, D, x0h, hdr_len);  // header bytes [0, hdrLen)
+    }
   } else {
     // ---- general header path (unusual csum offsets): byte-exact replay of
     // the reference's write order on the chunk (destination coordinates)
@@ -1139,12 +1221,355 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   }
 }
 
+// ---------------------------------------------------------------------------
+// Job staged whole in LDS (round 5): one workgroup of NW waves per job.
+//
+// gso_rows_kernel's payload loads wait on a dependent chain: the job
+// descriptor, then the virtio header and header chunks, then the verdict and
+// the segment geometry; only then does a row know which bytes to load
+// (≈ 4.7 µs of a one-stream cfg4 launch).  Here the payload
+// loads depend on the descriptor alone: every wave issues, right after its
+// header loads, LDS-DMA loads (global_load_lds_dwordx4) of its share of the
+// job's 16-byte chunks into a 65-KiB LDS image of the job, whatever the
+// geometry turns out to be.  The head (verdict, segment count, job-constant
+// sums) runs while those loads are in flight; then one vmcnt(0) + barrier,
+// and every row streams its segments out of LDS through the same consume /
+// finish code as the register path (dword-aligned 16-byte windows, shifted to
+// the destination phase, summed, stored; header chunk last).  So every input
+// byte is read from HBM once, by one load issued at the start of the launch.
+//
+// A job larger than the image (> 65,545 bytes at a 15-byte phase) streams
+// its rows from HBM as gso_rows_kernel does; every job that is not clean
+// takes the decoded path (decoded_rows) with NW * 4 rows per group.
+constexpr int kVmcnt0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15): gfx9 encoding, loads / stores only
+constexpr int kImgBytes = 66560;  // 4,160 chunks: a 65,545-byte job ([virtio hdr | 65,535 B]) at any 16-B phase
+
+// 16 bytes at the 4-byte aligned LDS offset o of the image (two ds_read2_b32).
+__device__ __forceinline__ uint4 img16(const uint8_t* img, int o) {
+  typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+  const u32x4a4 t = *reinterpret_cast<const u32x4a4*>(__builtin_assume_aligned(img + o, 4));
+  return make_uint4(t.x, t.y, t.z, t.w);
+}
+__device__ __forceinline__ uint32_t img4(const uint8_t* img, int o) {
+  return *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(img + o, 4));
+}
+
+// load_windows from the LDS image (job byte x at image offset ibias + x).
+// Unlike the HBM form, windows outside the row's payload bytes [lo, hi) are
+// read too (from LDS, no memory traffic) and not zeroed: consume_batch masks
+// every byte of a chunk outside [hdrLen, pktLen) -- the bytes such a window
+// contributes -- out of every sum and store.  Offsets below the image (a
+// window before the payload) clamp to 0; the image array has room for every
+// window past the job's end (>= 1,552 bytes of slack, gso_lds_kernel).
+template <int U>
+__device__ __forceinline__ void img_windows(const uint8_t* img, int ibias, int aoff, int k0, int r, uint4 (&A)[U],
+                                            uint32_t& E) {
+  const int o0 = ibias + aoff + 16 * (k0 + r);
+#pragma unroll
+  for (int u = 0; u < U; ++u) A[u] = img16(img, max(o0 + 256 * u, 0));
+  E = img4(img, max(ibias + aoff + 16 * (k0 + 16 * U), 0));  // used by lane 15 only
+}
+
+template <int U>
+__device__ __forceinline__ void stream_row_img(const uint8_t* img, int ibias, const uint8_t* rb, int i, int gso,
+                                               int hdr_len, int plen, int dalign, uint8_t* dbase, int r,
+                                               uint32_t& acc, RowOut& ro) {
+  const RowSrc g = row_src(rb, i, gso, hdr_len, plen, dalign);
+  acc = 0;
+  for (int k0 = 0; k0 < g.nk; k0 += 16 * U) {
+    uint4 A[U];
+    uint32_t E;
+    img_windows<U>(img, ibias, g.aoff, k0, r, A, E);
+    consume_batch_img<U>(A, E, k0, g, hdr_len, dalign, dbase, r, acc, ro);
+  }
+}
+
+// The head's results, published by wave 0 through LDS.
+struct LdsHead {
+  int32_t clean;  // 1: the row-streaming path (a clean job, gso_rows_kernel's criterion)
+  int32_t type, ipv, hdr_len, gso, cs, co, plen;
+  uint32_t ip_base, l4_base, tflags, id0, seq0;
+};
+
+#ifndef WGCS_GSO_LDS_WAVES
+#define WGCS_GSO_LDS_WAVES 8
+#endif
+// One workgroup of NW waves per job.  Wave 0 issues the header loads, then
+// every wave its share of the LDS-DMA loads of the whole job; wave 0 runs the
+// head (verdict, segment count, job-constant header sums) while they are in
+// flight and publishes it through LDS; one vmcnt(0) + barrier; then every row
+// streams its segments out of the image (header chunks read from it as well)
+// with write-through full-chunk stores: the segment stores follow the loads in
+// this kernel, so the lines go to HBM while the rows still work instead of
+// in one end-of-kernel writeback of every segment (≈ 17 MB for cfg4).
+template <int NW, int U, bool NT>
+__global__ __launch_bounds__(NW * 64) void gso_lds_kernel(const uint8_t* __restrict__ arena,
+                                                           const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
+                                                           uint8_t* __restrict__ out, uint32_t out_stride,
+                                                           const GsoOutPos* __restrict__ outpos, uint32_t offset,
+                                                           uint32_t room, int32_t* __restrict__ sizes,
+                                                           int32_t* __restrict__ count, int32_t* __restrict__ status) {
+  constexpr int ROWS = NW * 4;                                        // 16-lane rows per workgroup
+  constexpr int kIters = (kImgBytes / 16 + NW * 64 - 1) / (NW * 64);  // LDS-DMA instructions per wave
+  constexpr int kArr = kIters * NW * 64 * 16;                         // every slot a DMA writes
+  static_assert(kArr >= kImgBytes + 1552, "image slack for the windows past a job's end");
+  __shared__ __attribute__((aligned(16))) uint8_t img[kArr];
+  __shared__ LdsHead hd;
+#ifdef WGCS_GSO_STAMPS  // timing-only build (scripts/probe_gso_stamps.py, LDS kernel: NWAVES=NW)
+  uint64_t stp[5] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0};
+#endif
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15;
+  const int wv = threadIdx.x >> 6;
+  const uint32_t jb = blockIdx.x;
+  const wgcs_gso_job job = jobs[jb];
+  const uint8_t* vb = arena + job.off;
+  const uint32_t jlen = job.len;
+  const uint8_t* rb = vb + 10;
+  const uint64_t slot0 = (uint64_t)jb * max_segs;
+  uint64_t obase = slot0 * out_stride;
+  uint32_t opitch = out_stride;
+  uint32_t tails = 1;
+  if (outpos) {
+    obase = outpos[jb].base;
+    opitch = outpos[jb].pitch;
+    tails = outpos[jb].flags & kOutPosTails;
+  }
+  const int ibias = (int)((uintptr_t)vb & 15u);
+  const int nch = (int)((jlen + (uint32_t)ibias + 15u) >> 4);
+  const bool use_img = jlen >= 14 && nch <= kImgBytes / 16;  // block-uniform
+  const bool raw = (job.flags & WGCS_GSO_JOB_RAW) != 0;
+  // ---- wave 0: header chunks (as gso_rows_kernel) and the virtio header +
+  // readBuf[0] (16 bytes from the dword holding vb[0], range-checked: zeros
+  // past the job), issued ahead of its bulk loads so that the head waits for
+  // them alone (a counted vmcnt)
+  const int hph = (int)((uintptr_t)rb & 3u);
+  const uint8_t* hbase = rb - hph;
+  const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(hbase), (short)0, (int)(jlen + 3u) - (int)(hbase - vb), 0x00020000);
+  const int sh = (int)((uintptr_t)vb & 3u);
+  uint4 H0 = make_uint4(0, 0, 0, 0), w = make_uint4(0, 0, 0, 0);
+  if (wv == 0) {
+    H0 = bld16<false>(hrs, 16 * r);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(vb - sh), (short)0, (int)(jlen + 3u + (uint32_t)sh), 0x00020000);
+    w = bld16<false>(vrs, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the header loads ahead of the bulk loads
+  // ---- every wave: its share of the whole job into the LDS image.  Chunk q
+  // = the aligned 16 bytes at (vb & ~15) + 16 q, image offset 16 q (job byte x
+  // at ibias + x); an aligned chunk holding a job byte lies in that byte's
+  // page.  kIters instructions per wave unconditionally, through a
+  // range-checked resource over the job's chunks (loads past it are dropped;
+  // a job too large for the image gets an empty range): a fixed count of
+  // loads behind wave 0's header loads.
+  {
+    const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(vb - ibias), (short)0, use_img ? 16 * nch : 0, 0x00020000);
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int q0 = (it * NW + wv) * 64;  // this wave-instruction's first chunk (1 KiB of LDS)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(irs, (__attribute__((address_space(3))) void*)(img + 16 * q0), 16,
+                                               16 * (q0 + lane), 0, 0, NT ? 2 : 0);
+    }
+  }
+  // ---- wave 0: the head, while the bulk loads are in flight
+  if (wv == 0) {
+    // the virtio header words become scalars only here, behind the bulk loads
+    // (a wave-uniform load's value is otherwise moved into SGPRs at the load,
+    // with a vmcnt(0) in front of every bulk load)
+    uint4 wq = w;
+    asm volatile("" : "+v"(wq.x), "+v"(wq.y), "+v"(wq.z), "+v"(wq.w));
+    wq = make_uint4((uint32_t)ufl((int)wq.x), (uint32_t)ufl((int)wq.y), (uint32_t)ufl((int)wq.z),
+                    (uint32_t)ufl((int)wq.w));
+    uint32_t t1 = 0, hl = 0, g = 0, c = 0, o = 0, b0 = 0;
+    if (jlen >= 14) {
+      const uint64_t lo = ((uint64_t)wq.y << 32) | wq.x, hi = ((uint64_t)wq.w << 32) | wq.z;
+      const uint64_t v0 = sh ? (lo >> (8 * sh)) | (hi << (64 - 8 * sh)) : lo;
+      const uint64_t v1 = hi >> (8 * sh);
+      t1 = (uint32_t)(v0 >> 8) & 0xFFu;
+      hl = (uint32_t)(v0 >> 16) & 0xFFFFu;
+      g = (uint32_t)(v0 >> 32) & 0xFFFFu;
+      c = (uint32_t)(v0 >> 48) & 0xFFFFu;
+      o = (uint32_t)v1 & 0xFFFFu;
+      b0 = (uint32_t)(v1 >> 16) & 0xFFu;
+    }
+    const int plen_s = jlen > 10 ? (int)jlen - 10 : 0;
+    const int type_s = raw ? ((t1 == GSO_TCPV4 || t1 == GSO_TCPV6) ? (int)t1 : GSO_UDP_L4) : (int)t1;
+    const int ipv_s = raw ? ((job.flags & WGCS_GSO_JOB_V6) ? 6 : 4) : (int)(b0 >> 4);
+    const bool tcp_s = type_s != GSO_UDP_L4;
+    const bool ok_s = jlen >= 14 && g != 0 && (type_s == GSO_TCPV4 || type_s == GSO_TCPV6 || type_s == GSO_UDP_L4) &&
+                      ((ipv_s == 4 && type_s != GSO_TCPV6) || (ipv_s == 6 && type_s != GSO_TCPV4));
+    const int gso_s = (int)g, cs_s = (int)c, co_s = (int)o;
+    const int hdr_s = (raw || tcp_s) ? (int)hl : ((cs_s + 8) & 0xFFFF);
+    const int ca_s = (cs_s + co_s) & 0xFFFF;
+    const int pkt0_s = hdr_s + min(gso_s, plen_s - hdr_s);
+    const bool clean_s = ok_s && hdr_s < plen_s && cs_s >= (ipv_s == 4 ? 20 : 40) && ca_s + 2 <= hdr_s &&
+                         hdr_s <= kMaxHdrLen && (raw || !tcp_s || (hdr_s - cs_s >= 20 && hdr_s - cs_s <= 60)) &&
+                         fast_header(cs_s, hdr_s, ca_s, tcp_s) && (uint32_t)pkt0_s <= room;
+    uint4 Q;
+    {
+      const uint32_t nx = row_next(H0.x);
+      Q = make_uint4(__builtin_amdgcn_alignbyte(H0.y, H0.x, hph), __builtin_amdgcn_alignbyte(H0.z, H0.y, hph),
+                     __builtin_amdgcn_alignbyte(H0.w, H0.z, hph), __builtin_amdgcn_alignbyte(nx, H0.w, hph));
+    }
+    bool clean = clean_s;
+    if (clean && tcp_s && !raw) {  // the TCP data offset decides hdrLen (tun.go:601-614)
+      const int th = (int)((qbyte(Q, cs_s + 12) >> 4) * 4);
+      clean = ((cs_s + th) & 0xFFFF) == hdr_s;
+    }
+    uint32_t ip_base = 0, l4_base = 0, tflags = 0, id0 = 0, seq0 = 0;
+    if (ufl(clean ? 1 : 0)) {
+      if (lane == 0) {  // the checks can only end in the segment count here (gso_rows_kernel)
+        const int nfull_s = (plen_s - hdr_s + gso_s - 1) / gso_s;
+        const bool many = nfull_s > (int)max_segs;
+        count[jb] = many ? (int)max_segs - 1 : nfull_s;
+        status[jb] = many ? WGCS_ERR_TOO_MANY_SEGMENTS : 0;
+      }
+      // job-constant header sums (as gso_rows_kernel)
+      const int cs = cs_s, hdr_len = hdr_s, ipv = ipv_s;
+      const int x0 = 16 * r;
+      const int vlo = cs + 4, vhi = tcp_s ? cs + 8 : cs + 6;
+      const int ca = ca_s;
+      if (ipv == 4) {
+        const uint32_t m = byte_bits16(-x0, cs - x0) & ~byte_bits16(2 - x0, 6 - x0) & ~byte_bits16(10 - x0, 12 - x0);
+        ip_base = (uint32_t)ufl((int)bswap16(fold32_16(row16_sum_u32(add4_masked(0u, Q, m, false)))));
+      }
+      uint32_t ml4 = byte_bits16(cs - x0, hdr_len - x0) & ~byte_bits16(ca - x0, ca + 2 - x0) &
+                     ~byte_bits16(vlo - x0, vhi - x0);
+      if (tcp_s) ml4 &= ~byte_bits16(cs + 13 - x0, cs + 14 - x0);
+      const int a_lo = ipv == 4 ? 12 : 8, a_hi = ipv == 4 ? 20 : 40;
+      uint32_t s4 = add4_masked(0u, Q, ml4, false);
+      s4 = add4_masked(s4, Q, byte_bits16(a_lo - x0, a_hi - x0), (cs & 1) != 0);
+      uint32_t t4 = fold32_16(row16_sum_u32(s4));
+      if ((cs & 1) == 0) t4 = bswap16(t4);
+      if (tcp_s) tflags = qbyte(Q, cs + 13);
+      l4_base = (uint32_t)ufl((int)t4) + (tflags & ~0x09u);
+      if (ipv == 4) {
+        const uint32_t b45 = qdw(Q, 1);
+        id0 = ((b45 & 0xFFu) << 8) | ((b45 >> 8) & 0xFFu);
+      }
+      if (tcp_s) seq0 = __builtin_bswap32(qle32(Q, vlo));
+    }
+    if (lane == 0) {
+      hd.clean = clean ? 1 : 0;
+      hd.type = type_s;
+      hd.ipv = ipv_s;
+      hd.hdr_len = hdr_s;
+      hd.gso = gso_s;
+      hd.cs = cs_s;
+      hd.co = co_s;
+      hd.plen = plen_s;
+      hd.ip_base = ip_base;
+      hd.l4_base = l4_base;
+      hd.tflags = tflags;
+      hd.id0 = id0;
+      hd.seq0 = seq0;
+    }
+  }
+#ifdef WGCS_GSO_STAMPS
+  stp[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+  // ---- every wave's bulk loads have landed (the compiler's own s_waitcnt,
+  // not inline asm: its wait-count pass then knows no LDS-DMA is pending and
+  // puts no vmcnt(0) -- which would also wait for the row's earlier stores --
+  // in front of the image reads of the row loop); the barrier publishes the
+  // image and the head
+  __builtin_amdgcn_s_waitcnt(kVmcnt0);
+  lds_barrier();
+#ifdef WGCS_GSO_STAMPS
+  stp[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+  if (ufl(hd.clean)) {
+    const int type = ufl(hd.type), ipv = ufl(hd.ipv), hdr_len = ufl(hd.hdr_len), gso = ufl(hd.gso);
+    const int cs = ufl(hd.cs), co = ufl(hd.co), plen = ufl(hd.plen);
+    const uint32_t ip_base = (uint32_t)ufl((int)hd.ip_base), l4_base = (uint32_t)ufl((int)hd.l4_base);
+    const uint32_t tflags = (uint32_t)ufl((int)hd.tflags), id0 = (uint32_t)ufl((int)hd.id0);
+    const uint32_t seq0 = (uint32_t)ufl((int)hd.seq0);
+    auto has_seg = [&](int i) { return i < (int)max_segs && hdr_len + (int64_t)i * gso < plen; };
+    // readBuf[16r, 16r + 16): from the image, or (a job too large for it)
+    // from HBM as gso_rows_kernel reads it
+    uint4 Q;
+    if (use_img) {
+      const int dq = ibias + 10 + 16 * r, s = dq & 3;
+      const uint4 T = img16(img, dq - s);
+      const uint32_t T4 = img4(img, dq - s + 16);
+      Q = make_uint4(__builtin_amdgcn_alignbyte(T.y, T.x, s), __builtin_amdgcn_alignbyte(T.z, T.y, s),
+                     __builtin_amdgcn_alignbyte(T.w, T.z, s), __builtin_amdgcn_alignbyte(T4, T.w, s));
+    } else {
+      const uint4 Hq = bld16<false>(hrs, 16 * r);
+      const uint32_t nx = row_next(Hq.x);
+      Q = make_uint4(__builtin_amdgcn_alignbyte(Hq.y, Hq.x, hph), __builtin_amdgcn_alignbyte(Hq.z, Hq.y, hph),
+                     __builtin_amdgcn_alignbyte(Hq.w, Hq.z, hph), __builtin_amdgcn_alignbyte(nx, Hq.w, hph));
+    }
+    // write-through stores through a resource over the job's output region
+    // when every row offset fits it (block-uniform; else plain stores)
+    // (based at out + obase rounded down to 16 bytes: every row's dbase lies
+    // at a non-negative 16-byte multiple from it)
+    const bool wt = WGCS_GSO_WT && (uint64_t)max_segs * opitch + offset < 0x7FFF0000ull;
+    uint8_t* const obase16 = out + obase - ((uintptr_t)(out + obase) & 15u);
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(obase16, (short)0, 0x7FFFFFFF, 0x00020000);
+    for (int i = wv * 4 + (lane >> 4); has_seg(i); i += ROWS) {  // row-uniform
+      uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
+      const int dalign = (int)((uintptr_t)dst & 15u);
+      uint8_t* dbase = dst - dalign;
+      uint32_t acc = 0;
+      if (use_img) {
+        RowOut ro;
+        ro.keep = make_uint4(0, 0, 0, 0);
+        ro.rs = ors;
+        ro.dro = (int)(dbase - obase16);
+        ro.wt = wt;
+        stream_row_img<U>(img, ibias, rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, ro);
+        finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
+                   tflags, id0, seq0, &sizes[slot0 + (uint32_t)i], &ro);
+      } else {
+        stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen));
+        finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
+                   tflags, id0, seq0, &sizes[slot0 + (uint32_t)i]);
+      }
+    }
+#ifdef WGCS_GSO_STAMPS
+    stp[3] = __builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stp[4] = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && max_segs >= 128 && wv < 12) {
+      int32_t* sp = sizes + slot0 + 64 + wv * 5;
+      for (int k = 0; k < 5; ++k) sp[k] = (int32_t)(uint32_t)stp[k];
+    }
+#endif
+  } else {
+    // every other job: the decoded path, NW * 4 rows per group (the image's
+    // loads have drained above, so no LDS-DMA write can land after the
+    // workgroup retires)
+    for (int grp = 0;; ++grp) {  // block-uniform
+      const int i = grp * ROWS + wv * 4 + (lane >> 4);
+      uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
+      const int live = decoded_rows<U, NT>(vb, jlen, job.flags, room, max_segs, i, grp == 0, &count[jb], &status[jb],
+                                           out + obase + offset, dst, &sizes[slot0], tails);
+      lds_barrier();
+      if ((int64_t)(grp + 1) * ROWS >= (int64_t)ufl(live)) break;
+    }
+  }
+}
+
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs, uint8_t* out,
                                   uint32_t out_stride, uint32_t offset, uint32_t max_segs, int32_t* sizes,
                                   int32_t* count, int32_t* status, hipStream_t s, const GsoOutPos* outpos,
                                   uint32_t room) {
   if (n_jobs == 0 || max_segs == 0) return hipSuccess;
   if (!outpos) room = out_stride > offset ? out_stride - offset : 0;
+  // WGCS_GSO_KERNEL=rows selects the round-4 grid (A/B builds and probes)
+  static const int use_rows = [] {
+    const char* e = getenv("WGCS_GSO_KERNEL");
+    return e && e[0] == 'r' ? 1 : 0;
+  }();
+  if (!use_rows) {
+    constexpr int NW = WGCS_GSO_LDS_WAVES;
+    hipLaunchKernelGGL((gso_lds_kernel<NW, WGCS_GSO_U, true>), dim3(n_jobs), dim3(NW * 64), 0, s, arena, jobs,
+                       max_segs, out, out_stride, outpos, offset, room, sizes, count, status);
+    return hipGetLastError();
+  }
   // 16 segments (4 waves) per block and group; a few blocks per job, each
   // looping over its groups (a 65,535-B read at MSS 1460 has 3 groups)
   const uint32_t ngroups = (max_segs + 15) / 16;
