@@ -20,7 +20,7 @@
 #include <unordered_map>
 #include <vector>
 
-#include "wgcs_kernels.h"
+#include "wgcs_host.h"
 
 namespace wgcs {
 namespace gro {

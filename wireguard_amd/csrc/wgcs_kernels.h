@@ -5,159 +5,23 @@
 #include <stdint.h>
 
 #include "../../include/wgcsum.h"
+#include "wgcs_host.h"
 
 namespace wgcs {
-
-struct LaunchTuning {
-  int blocks_per_cu = 16;  // 256-thread blocks per CU for the grid-stride grid
-  int lanes_per_pkt = 32;  // 16: one DPP row per packet (4 per wave); 32: half wave (2 per wave); 64: one wave
-  int unroll = 4;          // 16-byte loads in flight per lane per iteration
-  int nt = 1;              // non-temporal (streaming) loads: each byte is read once
-  int align = 16;          // chunk grid origin: packet start rounded down to this many bytes
-  int xcd = 1;             // XCD-aware block order (each XCD streams contiguous eighths)
-};
 
 hipError_t launch_checksum_batch(int mode, unsigned flags, uint8_t* arena, const wgcs_pkt* pkts,
                                  const uint64_t* init, uint32_t n, void* out, hipStream_t s, int num_cu,
                                  const LaunchTuning& tune);
-
-// Optional packed output layout: segment i of job j at out + base + i*pitch
-// (+ offset); pitch must hold the job's largest segment.  The room checks
-// (handleVirtioRead's bufs element length) then use `room` instead of
-// out_stride - offset.  Without kOutPosTails the kernel writes the packets
-// only: gsoSplit's header writes that land past a segment's end (a field
-// beyond hdrLen) are skipped, so a pitch sized for the packets is never
-// overrun.  With it (the caller's buffers staged into the region, a pitch of
-// at least gso_field_reach) they are written as into fixed slots.
-enum : uint32_t { kOutPosTails = 1 };
-struct GsoOutPos {
-  uint64_t base;
-  uint32_t pitch;
-  uint32_t flags;  // kOutPosTails
-};
-// Packed-layout pitch and segment bound of one job ([10-byte virtio header |
-// packet], n bytes) from its virtio header and job flags: every segment
-// gso_rows_kernel can write for it fits in `pitch` (a segment is at most
-// min(len, hdrLen + gsoSize) bytes; hdrLen is the caller's for RAW jobs and at
-// most csumStart + 60 after handleVirtioRead's recompute), and it writes at
-// most `segs` of them; 0/0 when it writes none.
-inline void gso_out_layout(const uint8_t* vb, size_t n, uint32_t jflags, uint32_t max_segs, uint32_t* pitch,
-                           uint32_t* segs) {
-  *pitch = 0;
-  *segs = 0;
-  if (n <= 10) return;  // short buffer / empty packet: nothing written
-  const size_t plen = n - 10;
-  const size_t gso = (size_t)vb[4] | ((size_t)vb[5] << 8);
-  const bool raw = (jflags & WGCS_GSO_JOB_RAW) != 0;
-  if (!raw && vb[1] == 0) {  // GSO_NONE: the packet itself
-    *pitch = (uint32_t)((plen + 15) & ~(size_t)15);
-    *segs = 1;
-    return;
-  }
-  const size_t cs = (size_t)vb[6] | ((size_t)vb[7] << 8);
-  const size_t hdr = raw ? ((size_t)vb[2] | ((size_t)vb[3] << 8)) : cs + 60;
-  size_t seg = hdr + gso < plen ? hdr + gso : plen;
-  if (seg < 16) seg = 16;
-  *pitch = (uint32_t)((seg + 15) & ~(size_t)15);
-  const size_t nseg = gso ? (plen + gso - 1) / gso + 1 : (size_t)max_segs;
-  *segs = (uint32_t)(nseg < max_segs ? nseg : max_segs);
-}
-
-// Bytes of bufs[i][offset:] that segment i (pkt_len bytes, `last` or not) of
-// the job vb ([10-byte virtio header | packet], n bytes) writes: the packet
-// plus gsoSplit's fixed-position header writes (gro.go:1419-1488 -- IPv4
-// [2:12) or IPv6 [4:6), seq / UDP length at csumStart+4, the TCP flags byte on
-// non-last segments, the checksum field; u16 positions).  A shorter Go slice
-// panics, so the host entry points report OUT_OF_RANGE there.  GSO_NONE
-// (handleVirtioRead semantics) writes the packet only.
-inline size_t gso_split_need(const uint8_t* vb, size_t n, uint32_t jflags, size_t pkt_len, bool last) {
-  if (n < 10) return pkt_len;
-  const bool raw = (jflags & WGCS_GSO_JOB_RAW) != 0;
-  const uint8_t t = vb[1];
-  if (!raw && t == 0) return pkt_len;
-  const bool v4 = raw ? (jflags & WGCS_GSO_JOB_V6) == 0 : (n > 10 && (vb[10] >> 4) == 4);
-  const bool tcp = t == 1 || t == 4;
-  const uint16_t cs = (uint16_t)(vb[6] | (vb[7] << 8)), co = (uint16_t)(vb[8] | (vb[9] << 8));
-  size_t need = pkt_len > (size_t)(v4 ? 12 : 6) ? pkt_len : (size_t)(v4 ? 12 : 6);
-  size_t f = (size_t)(uint16_t)(cs + 4) + (tcp ? 4 : 2);
-  if (f > need) need = f;
-  if (tcp && !last && (f = (size_t)(uint16_t)(cs + 13) + 1) > need) need = f;
-  if ((f = (size_t)(uint16_t)(cs + co) + 2) > need) need = f;
-  return need;
-}
-
-// gsoSplit's fixed-position header writes' reach for job vb: the last byte + 1
-// of IPv4 [2:12) / IPv6 [4:6), seq or UDP length, the flags byte (non-last
-// segments) and the checksum field.
-inline size_t gso_field_reach(const uint8_t* vb, size_t n, uint32_t jflags) {
-  return gso_split_need(vb, n, jflags, 0, false);
-}
-
-// Does gsoSplit's result for job vb involve bytes of bufs[i] other than the
-// segments it produces?  Either a header write can land past a segment's end
-// (a field beyond the smallest hdrLen the job can have), or the IPv4 id update
-// reads bufs[i][4:6] (an IP header shorter than 6 bytes, gro.go:1426-1431).
-// Host entry points then stage the caller's buffers through the kernel.
-// Never for a well-formed TCP / UDP header (every field inside hdrLen).
-inline bool gso_touches_caller_bytes(const uint8_t* vb, size_t n, uint32_t jflags) {
-  if (n <= 10) return false;
-  const bool raw = (jflags & WGCS_GSO_JOB_RAW) != 0;
-  const uint8_t t = vb[1];
-  if (!raw && t == 0) return false;  // GSO_NONE: the packet only
-  const bool v4 = raw ? (jflags & WGCS_GSO_JOB_V6) == 0 : (vb[10] >> 4) == 4;
-  const bool tcp = t == 1 || t == 4;
-  const size_t cs = (size_t)vb[6] | ((size_t)vb[7] << 8);
-  if (v4 && cs <= 5) return true;
-  size_t lb;  // hdrLen's lower bound (handleVirtioRead's u16 recompute may wrap: then 0)
-  if (raw) lb = (size_t)vb[2] | ((size_t)vb[3] << 8);
-  else if (tcp) lb = cs + 60 <= 0xFFFF ? cs + 20 : 0;
-  else lb = cs + 8 <= 0xFFFF ? cs + 8 : 0;
-  return gso_field_reach(vb, n, jflags) > lb;
-}
 
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs,
                                   uint8_t* out, uint32_t out_stride, uint32_t offset, uint32_t max_segs,
                                   int32_t* sizes, int32_t* count, int32_t* status,
                                   hipStream_t s, const GsoOutPos* outpos = nullptr, uint32_t room = 0);
 
-// One coalesced GRO output (applyTCPCoalesce / applyUDPCoalesce item).
-struct GroItem {
-  uint64_t out_off;   // [10-byte virtio header | packet] written at out + out_off
-  uint32_t head_off;  // stage offset of the head packet (header source)
-  uint32_t pkt_len;   // final IP packet length
-  uint32_t seg_first, seg_count;  // payload segments in segs[]
-  uint16_t gso_size;
-  uint8_t iph, l4h;
-  uint8_t kind;  // GRO_KIND_*
-  uint8_t pad[7];
-};
-struct GroSeg {
-  uint32_t src_off, len;  // stage offset / length of one payload piece
-  uint32_t dst_off, pad;  // output offset of the piece (host-computed: pieces copy in parallel)
-};
-// RAW: the coalesced bytes only (head packet header + PSH, no apply*, no virtio
-// header) -- handleGRO stopped at an invalid offset before applyTCPCoalesce.
-enum : uint8_t { GRO_KIND_V6 = 1, GRO_KIND_UDP = 2, GRO_KIND_PSH = 4, GRO_KIND_RAW = 8 };
-
 // Device-resident batch of handleGRO calls (gro_batch_kernels.hip).
 hipError_t launch_gro_batch(uint8_t* arena, wgcs_gro_buf* bufs, const wgcs_gro_call* calls, uint32_t n_calls,
                             int32_t* status, int32_t* n_write, int32_t* to_write, hipStream_t s);
 
-// Write stager around the batched handleGRO (wstager.cpp): packets staged
-// back to back are moved into their Go-sized slices of the device arena, and
-// after the handleGRO launch the toWrite images of each call are packed into
-// that call's output region.  Source and destination of both copies share
-// their phase mod 16, so both move whole aligned 16-byte chunks.
-struct WsMove {
-  uint64_t src, dst;    // 16-byte aligned source (stage offset, or a device-visible address) / arena offset
-  uint32_t n16, flags;  // 16-byte chunks; WS_MOVE_ABS: src is an address (pinned host memory)
-};
-enum : uint32_t { WS_MOVE_ABS = 1 };
-struct WsOut {
-  uint64_t base;  // the call's output region (16-byte aligned)
-  uint32_t room;  // its size in bytes
-  uint32_t pad;
-};
 hipError_t launch_ws_scatter(const uint8_t* stage, uint8_t* arena, const WsMove* mv, uint32_t n, hipStream_t s);
 hipError_t launch_ws_gather(const uint8_t* arena, const wgcs_gro_buf* bufs, const wgcs_gro_call* calls,
                             const WsOut* outs, uint32_t n_calls, int32_t* status, const int32_t* n_write,
