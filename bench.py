@@ -446,10 +446,11 @@ def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, ro
         evs = (e0 if use_events else None, e1 if use_events else None)
         if bell is not None and gated:
             bell[0] = 0
-            # every launch stream waits on the bell itself: streams[1:] also
-            # wait on e0 when the events are on, but without events nothing
-            # else would hold them before the clock starts
-            for s in strm[:ns]:
+            # with the bracket events on, streams[1:] wait on e0, recorded on
+            # stream 0 behind the bell; without events nothing else would hold
+            # them before the clock starts, so each waits on the bell itself
+            # 
+            for s in (strm[:1] if use_events else strm[:ns]):
                 dev.stream_wait_flag(s, bell, 1)
             try:
                 dev.checksum_batches(mode, bl, strm[:ns], *evs)

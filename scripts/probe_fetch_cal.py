@@ -33,7 +33,13 @@ for k in range(5):
 for stride, off, ln in ((65552, 16, 1488), (65552, 16, 1448), (65552, 16, 1500), (65552, 16, 60), (65536, 0, 1452)):
     a0 = [(arena.data_ptr() + p * stride + off) & ~15 for p in range(0, npk)]
     span = sum(((arena.data_ptr() + p * stride + off + ln + 15) & ~15) - a for p, a in zip(range(npk), a0))
-    rec["rows"][f"{ln}@{stride}+{off}"] = {"len_bytes": npk * ln, "span_bytes": span}
+    # the bytes of the 128-B (and 64-B) lines the rows touch: a read's floor
+    # at line granularity (round 5: the sized-request counters, scripts/pmc_sized.py)
+    base = arena.data_ptr()
+    lines128 = sum((((base + p * stride + off + ln + 127) >> 7) - ((base + p * stride + off) >> 7)) for p in range(npk))
+    lines64 = sum((((base + p * stride + off + ln + 63) >> 6) - ((base + p * stride + off) >> 6)) for p in range(npk))
+    rec["rows"][f"{ln}@{stride}+{off}"] = {"len_bytes": npk * ln, "span_bytes": span, "line128_bytes": 128 * lines128,
+                                         "line64_bytes": 64 * lines64}
     for k in range(5):
         L.cal_rows_launch(arena.data_ptr(), npk, stride, off, ln, out.data_ptr(), s)
 torch.cuda.synchronize()

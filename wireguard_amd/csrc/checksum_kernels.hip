@@ -9,7 +9,8 @@
 //
 // Design: the launched kernel is checksum_batch_kernel<MODE,
 // G = 32, U = 4, NT>: one G-lane group (half a wave64) per packet, two packets
-// per wave, persistent grid-stride over packets with an XCD-aware block order.
+// per wave, an XCD-aware block order, one pass of the grid over batches of up
+// to num_cu x 1,024 x 8 frames (grid-stride beyond that; round 5, wgcs_host.h).
 // Each lane streams 16-byte chunks of its packet with non-temporal
 // global_load_dwordx4 (U loads in flight per lane: 2 KiB per half-wave step,
 // so one iteration covers a 1500-B frame), masks only the head / checksum
@@ -179,7 +180,8 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
     const int rel0 = lo_all - (int)((pbase + (uintptr_t)lo_all) & amask);
     const int nch = hi_all > lo_all ? (hi_all - rel0 + 15) >> 4 : 0;
     int c_lo = min((hole_end - rel0 + 15) >> 4, nch);  // first unmasked chunk
-    int c_hi = max((hi_all - rel0) >> 4, c_lo);        // end of unmasked chunks
+    int c_hi = nch ? max((hi_all - rel0) >> 4, c_lo) : 0;  // end of unmasked chunks (none for an empty range:
+                                                             // with a 128-B origin rel0 may lie 127 B below it)
     const int n_edge = c_lo + (nch - c_hi);
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(pkt + rel0);
     uint32_t acc = 0;
@@ -187,12 +189,18 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
     int ce = sub < c_lo ? sub : c_hi + (sub - c_lo);
     uint4 ve = (sub < n_edge && rel0 + 16 * ce + 16 > lo_all) ? ld_chunk<NT>(src + ce) : make_uint4(0, 0, 0, 0);
     bool edge_pending = true;
-    for (int c0 = c_lo + sub; c0 < c_hi || edge_pending; c0 += G * U) {
+    // With a 128-byte chunk grid origin (amask 127) the interior iterations
+    // start on a line boundary too (c_it: c_lo rounded down to 8 chunks; the
+    // lanes below c_lo idle in the first one), so no 128-byte line is shared by
+    // two iterations of a row -- with non-temporal loads such a line can be
+    // evicted between them and read twice (round 5, profiles/r5_cfg5_traffic*)
+    const int c_it = amask >= 127u ? (c_lo & ~7) : c_lo;
+    for (int c0 = c_it + sub; c0 < c_hi || edge_pending; c0 += G * U) {
       uint4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int c = c0 + u * G;
-        v[u] = c < c_hi ? ld_chunk<NT>(src + c) : make_uint4(0, 0, 0, 0);
+        v[u] = (c < c_hi && c >= c_lo) ? ld_chunk<NT>(src + c) : make_uint4(0, 0, 0, 0);
       }
       if (edge_pending) {
         for (int e = sub;;) {  // rows with more than G edge chunks (long field offsets) loop
@@ -251,7 +259,9 @@ static hipError_t launch_mode(uint8_t* arena, const wgcs_pkt* pkts, const uint64
                               int inplace, hipStream_t s, int num_cu, const LaunchTuning& t) {
   const int ppb = (64 / t.lanes_per_pkt) * 4;  // packets per block per step
   long want = ((long)n + ppb - 1) / ppb;
+  want = (want + 7) & ~7L;  // a multiple of 8 keeps the XCD-aware order (blocks past n exit at once)
   long cap = (long)num_cu * t.blocks_per_cu;
+  cap = cap > 8 ? cap & ~7L : cap;
   const int grid = (int)(want < cap ? want : cap);
   const uint32_t amask = (uint32_t)(t.align >= 16 ? t.align : 16) - 1u;
   const int xcd = (t.xcd && grid % 8 == 0) ? 1 : 0;

@@ -87,6 +87,17 @@ __device__ __forceinline__ uint32_t be16g(const uint8_t* p) { return ((uint32_t)
 
 __device__ __forceinline__ uint32_t fnv(uint32_t h, uint32_t b) { return (h ^ b) * 16777619u; }
 
+// Orders one wave's LDS accesses across its lanes: the wave-cooperative walk
+// (run_flow_wave, tcp_gro_wave, append_run) hands LDS state from lane 0 to
+// every lane and back.  A wave's LDS operations execute in issue order; this
+// keeps the compiler from moving a lane's read above another lane's write to
+// a location it cannot prove aliased (a wavefront-scope acquire-release fence
+// emits no instruction, the wave barrier pins the schedule).  ADVICE r4.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // ---- the handleGRO loop over the precomputed fields (one thread per flow) ---
 
 struct Planner {
@@ -463,6 +474,7 @@ struct Planner {
         S.fnit[f] = (int16_t)nit;
         S.fl_tail[f] = nit ? S.fitem[base + nit - 1] : (int16_t)kNone;
       }
+      wave_lds_sync();
       return __builtin_amdgcn_readfirstlane(result);
     }
     {  // nit <= 64: one lane per item
@@ -512,6 +524,7 @@ struct Planner {
           S.fitem[base + np] = (int16_t)it;
         }
         if ((del >> lane) & 1ull) S.it_alive[it] = 0;
+        wave_lds_sync();  // the compaction, before lane 0 reads fitem below
       }
       if (dec) {
         const int d = __builtin_ctzll(dec);
@@ -537,6 +550,7 @@ struct Planner {
       S.fnit[f] = (int16_t)nit;
       S.fl_tail[f] = nit ? S.fitem[base + nit - 1] : (int16_t)kNone;
     }
+    wave_lds_sync();  // lane 0's coalesce / insert, before any lane reads the flow again
     return result;
   }
 
@@ -594,6 +608,7 @@ struct Planner {
         S.pnext[first ? c.stail : w + prev] = (int16_t)q;
         S.res[q] = R_COALESCED;
       }
+      wave_lds_sync();  // every member's piece links
       if (A) {  // the item after the run (only its last member may carry PSH or a short payload)
         const int L = 63 - __builtin_clzll(A);
         const int cnt = __builtin_popcountll(A);
@@ -637,12 +652,14 @@ struct Planner {
         load_tail(c, f);
         i = append_run<udp>(c, f, i, n_eff, lane, ubad);
         if (lane == 0) flush_tail(c);  // the item loop below reads the item from LDS
+        wave_lds_sync();
         c.dirty = false;
         if (i == kNone) break;
       }
       int res = R_INSERT;
       if constexpr (udp) {  // udpGRO's outcome for a packet that does not append: a new item (the flow's last)
         if (lane == 0) insert(i, f, (uint8_t)ubad);
+        wave_lds_sync();
       } else {
         // in a reordered flow the in-order fast path is tried again only after
         // the item loop appended to the flow's last item
@@ -652,6 +669,7 @@ struct Planner {
                                  : res == R_COALESCED && S.fl_tail[f] != kNone && S.stail[S.it_slot[S.fl_tail[f]]] == i;
       }
       if (lane == 0) S.res[i] = (uint8_t)res;
+      wave_lds_sync();
       i = S.fnext[i];
     }
   }

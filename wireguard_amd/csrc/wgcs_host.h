@@ -12,11 +12,19 @@
 namespace wgcs {
 
 struct LaunchTuning {
-  int blocks_per_cu = 16;  // 256-thread blocks per CU for the grid-stride grid
+  // 256-thread blocks per CU at most.  Round 5: 1,024, so a batch of up to 2M
+  // frames is one pass of the grid (every wave its own frames, no grid
+  // stride): with 32 passes (the old 16 per CU) the waves drift apart and the
+  // 128-byte line two neighbouring frames share was read twice, 5.6 % extra
+  // HBM reads on cfg5 (profiles/r5_traf2_*); one pass: 1.1 %, and 5 % faster
+  int blocks_per_cu = 1024;
   int lanes_per_pkt = 32;  // 16: one DPP row per packet (4 per wave); 32: half wave (2 per wave); 64: one wave
   int unroll = 4;          // 16-byte loads in flight per lane per iteration
   int nt = 1;              // non-temporal (streaming) loads: each byte is read once
-  int align = 16;          // chunk grid origin: packet start rounded down to this many bytes
+  // chunk grid origin: packet start rounded down to this many bytes.  Round 5:
+  // 128, and the interior iterations start on a line too, so no line is read
+  // by two iterations of a row (cfg3's 9000-B frames: 6.3 % -> 1.5 % extra reads)
+  int align = 128;
   int xcd = 1;             // XCD-aware block order (each XCD streams contiguous eighths)
 };
 
