@@ -79,6 +79,9 @@ def parse():
                     help="cfg4: output slots placed so that bufs[i][offset] starts on this many bytes (0: as allocated)")
     ap.add_argument("--gso-in-align", type=int, default=128,
                     help="cfg4: each read's buffer at a multiple of this many bytes in the arena (0: packed)")
+    ap.add_argument("--gro-buf-align", type=int, default=128,
+                    help="gro_device: buffers placed so that bufs[k][offset] starts on this many bytes (0: 16-byte "
+                         "multiples back to back)")
     ap.add_argument("--verify", action="store_true", help="check the GPU results against the synth ground truth")
     ap.add_argument("--no-strong", action="store_true",
                     help="cfg2: skip the configs[4] block (the 1M mixed batch split over the ranks, `cfg5_strong`)")

@@ -112,7 +112,7 @@ def test_recorded_rehearsal_lines_complete():
     profiles/r4_rehearse_gpus*.jsonl) are complete by the same check."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r4_rehearse_gpus*_gloo.jsonl")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[4-9]_rehearse_gpus*_gloo.jsonl")))
     if not files:
         pytest.skip("no rehearsal lines recorded yet")
     for fn in files:
@@ -122,6 +122,26 @@ def test_recorded_rehearsal_lines_complete():
                     line = json.loads(l)
                     assert line["n_gpus"] > 1
                     assert bench.line_problems(line) == [], fn
+
+
+def test_recorded_eight_rank_rehearsal():
+    """the driver's 8-GPU run is one-shot, so the 8-rank
+    line was rehearsed once on the 1-GPU box (`WGCS_DIST_BACKEND=gloo python
+    bench.py --gpus 8 --steps 20 --warmup 5`, 8 gloo ranks time-sharing
+    cuda:0, profiles/r5_rehearse_gpus8_gloo.jsonl): one complete line, every
+    rank's kernel time, the 1M batch split over all 8, and rank 0's CPU
+    baseline inside the run the other 7 ranks waited for at the barrier."""
+    fn = os.path.join(ROOT, "profiles", "r5_rehearse_gpus8_gloo.jsonl")
+    if not os.path.exists(fn):
+        pytest.skip("8-rank rehearsal not recorded yet")
+    lines = [json.loads(l) for l in open(fn) if l.startswith("{")]
+    assert len(lines) == 1
+    line = lines[0]
+    assert bench.line_problems(line) == []
+    assert line["n_gpus"] == 8 and line["config"]["dist"]["world_size"] == 8
+    assert len(line["roofline"]["kernel_ms_per_rank"]) == 8
+    assert len(line["cfg5_strong"]["packets_per_rank"]) == 8
+    assert line["cpu_baseline"]["value"] > 0
 
 
 def test_numa_helpers(tmp_path):

@@ -31,7 +31,7 @@
 // callers recycle bufs after the call, device/receive.go:500-505).
 //
 // Device arena layout of one staged buffer (16-byte aligned region R): the
-// packet at P = R + 32 + align16(offset) + phase, where phase is the packet's
+// packet at P = align128(R + 32 + align16(offset)) + phase, where phase is the packet's
 // address mod 16 in its source (0 for the packed stage, the caller's for
 // pinned pushes), so source and slice share their phase; the slice `off` =
 // P - offset holds cap bytes; 16+ bytes of pad on both sides.  The scatter and
@@ -70,8 +70,10 @@ struct WCall {  // one Tun.Write call
 // Output bytes reserved per packet: its write(2) image as whole aligned chunks
 // (align16(len + 10) + up to 15 bytes of phase) fits in 32 + align16(len).
 inline size_t out_need(size_t pl) { return 32 + al16(pl); }
-// Device arena bytes of one slice
-inline uint64_t arena_need(size_t offset, size_t cap) { return 64 + al16(offset) + al16(cap - offset); }
+// Device arena bytes of one slice (+112: the packet moved up to the next
+// 128-byte line, below)
+inline uint64_t arena_need(size_t offset, size_t cap) { return 64 + 112 + al16(offset) + al16(cap - offset); }
+inline uint64_t al128(uint64_t x) { return (x + 127) & ~(uint64_t)127; }
 
 struct WSlot {
   uint64_t id = 0;
@@ -345,7 +347,10 @@ int push_call(wgcs_wstager* ws, const uint8_t* const* bufs, const size_t* lens, 
       const size_t cap = std::min(caps[i], (size_t)offset + total);
       const uintptr_t hp = (uintptr_t)(bufs[i] + offset);  // the packet in host memory
       const uint64_t phase = pinned ? (uint64_t)(hp & 15u) : 0u;
-      const uint64_t pkt = s.arena + 32 + al16((size_t)offset) + phase;  // the packet in the arena
+      // the packet in the arena: on a 128-byte line (+ its source phase mod 16
+      // for a zero-copy push), so its reads and the appends behind it touch
+      // no more lines than its bytes need (round 5)
+      const uint64_t pkt = al128(s.arena + 32 + al16((size_t)offset)) + phase;
       wgcs_gro_buf& b = s.h_bufs[s.npk];
       b.off = pkt - (uint64_t)offset;
       b.len = (uint32_t)lens[i];

@@ -392,7 +392,14 @@ def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int =
     pkts = shape_batch(dev, shape)
     n = len(pkts)
     N = calls * n
-    stride = int(os.environ.get("WGCS_GRO_STRIDE", (CAP + 15) // 16 * 16))  # buffer k at k * stride
+    # Buffer k at shift + k * stride.  --gro-buf-align A (default 128): stride
+    # a multiple of A and the arena shifted so that every bufs[k][offset]
+    # starts on an A-byte line, as cfg4 places its slots (the reference's bufs
+    # are separate Go allocations at whatever address; here the device batch's
+    # layout is ours to choose).  0: back to back at 16-byte multiples.
+    align = int(getattr(args, "gro_buf_align", 0) or 16)
+    stride = int(os.environ.get("WGCS_GRO_STRIDE", (CAP + align - 1) // align * align))
+    shift = (align - OFFSET % align) % align
     W = (OFFSET + max(len(p) for p in pkts) + 31) // 16 * 16  # bytes restored per buffer
     img = np.zeros((n, W), np.uint8)
     for i, p in enumerate(pkts):
@@ -401,9 +408,9 @@ def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int =
     # rotated copies (each launch's packets alone exceed the 256 MiB MALL), at
     # most ~64 GiB of slices in all, at least 2 (consecutive launches overlap)
     R = max(2, min(rotate, (64 << 30) // (N * stride)))
-    arenas = [torch.empty(N * stride, dtype=torch.uint8, device="cuda") for _ in range(R)]
+    arenas = [torch.empty(N * stride + shift, dtype=torch.uint8, device="cuda") for _ in range(R)]
     gb = np.zeros(N, GRO_BUF_DTYPE)
-    gb["off"] = np.arange(N, dtype=np.uint64) * np.uint64(stride)
+    gb["off"] = np.arange(N, dtype=np.uint64) * np.uint64(stride) + np.uint64(shift)
     gb["len"] = np.tile(np.array([OFFSET + len(p) for p in pkts], np.uint32), calls)
     gb["cap"] = CAP
     d_bufs0 = torch.from_numpy(gb.view(np.uint8)).cuda()
@@ -423,7 +430,7 @@ def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int =
 
     def restore():
         for r in range(R):
-            arenas[r].view(N, stride)[:, :W].copy_(d_img)
+            arenas[r][shift: shift + N * stride].view(N, stride)[:, :W].copy_(d_img)
             d_bufs[r].copy_(d_bufs0)
         torch.cuda.synchronize()
 
@@ -505,6 +512,8 @@ def run_device(args, torch, dev, dist, rank, world, local, barrier, calls: int =
             "payload_bytes_per_step": payload,
             "rotated_copies": R,
             "streams": S,
+            "buffer_stride": stride,
+            "buf_align": align,
             "parallelism": f"replica{world} (one batch per GPU, no collective)",
             "gib_per_s": round(payload / per / 2**30, 3),
         },
