@@ -102,6 +102,14 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
     elapsed = shard.max_over_ranks(elapsed, dist)
     stream = streams[0]
     achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
+    if os.environ.get("WGCS_GSO_KERNEL", "")[:1] == "r":  # the round-4 grid (A/B)
+        kname = "gso_rows_kernel<6,true>"
+        grid = (f"({n_jobs}, {min((max_segs + 15) // 16, 3)}) blocks of 256: one block per (job, group lane), "
+                "looping over segment groups")
+    else:
+        kname = "gso_lds_kernel<8,6,true>"
+        grid = (f"{n_jobs} blocks of 512: one workgroup per read, the read staged whole in LDS by LDS-DMA, "
+                "16-lane rows stream its segments out")
     # calibration: a plain device-to-device copy of the super-packet bytes
     # (same read + write volume, same rotation) with the runtime's copy kernel
     with torch.cuda.stream(stream):
@@ -148,9 +156,9 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic.per_launch("gso_rows_kernel<6,true>", bytes_per_step),
-            "kernel": "gso_rows_kernel<6,true>",
-            "grid": f"({n_jobs}, {min((max_segs + 15) // 16, 3)}) blocks of 256: one block per (job, group lane), looping over segment groups",
+            "traffic": traffic.per_launch(kname, bytes_per_step),
+            "kernel": kname,
+            "grid": grid,
             "kernel_ms": round(kern_ms, 5),
             "kernel_ms_is": ("GPU time per launch over the timed region (HIP events on the launch streams)"
                              + (f"; {S} streams, consecutive launches overlap" if S > 1 else "")),
