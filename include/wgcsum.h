@@ -342,7 +342,10 @@ int wgcs_stager_result(wgcs_stager *st, uint64_t batch, int read_idx, int *statu
  * of wgcs_stager_result holds the packets only: for a read whose header
  * geometry writes past a segment's end or reads bufs[i][4:6] (an IPv4 header
  * shorter than 6 bytes), copy_out runs the read again through the per-call
- * path with these bufs, so that every byte matches (gro.go:1419-1488). */
+ * path with these bufs, so that every byte matches (gro.go:1419-1488).  That
+ * rerun is a synchronous GPU round trip under the context's lock; it runs on a
+ * copy of the read with the stager unlocked, so other calls on the stager do
+ * not wait for it. */
 int wgcs_stager_copy_out(wgcs_stager *st, uint64_t batch, int read_idx, uint8_t *const *bufs,
                          const size_t *buf_lens, int nbufs, int *sizes, int offset, int *n_out);
 

@@ -362,7 +362,7 @@ int wgcs_stager_copy_out(wgcs_stager* st, uint64_t batch, int read_idx, uint8_t*
   if ((uint32_t)nbufs != st->max_segs)
     return set_err(st->ctx, WGCS_ERR_INVALID_ARG, "copy_out: nbufs must equal the stager's max_segs");
   *n_out = 0;
-  std::lock_guard<std::mutex> g(st->mu);  // the slot cannot be recycled while its results are copied
+  std::unique_lock<std::mutex> g(st->mu);  // the slot cannot be recycled while its results are copied
   Slot* s = st->find(batch);
   if (!s || s->state == 1 || hipEventQuery(s->done) != hipSuccess) return WGCS_ERR_NOT_READY;
   if (read_idx < 0 || (uint32_t)read_idx >= s->n_reads) return WGCS_ERR_INVALID_ARG;
@@ -380,8 +380,13 @@ int wgcs_stager_copy_out(wgcs_stager* st, uint64_t batch, int read_idx, uint8_t*
     // packets (a field past a segment's end, or the IPv4 id update reading
     // bufs[i][4:6]): the batch kernel wrote the packets only; the read runs
     // again on the GPU through the per-call path, with these buffers staged.
+    // That is a synchronous round trip: it runs on a copy of the read, with
+    // the stager unlocked, so submit / wait / result calls are not held up
+    // behind it.
+    std::vector<uint8_t> read(vb, vb + vlen);
+    g.unlock();
     int st2 = 0, n2 = 0;
-    const int rc = gso_split_staged(st->ctx, vb, vlen, 0, bufs, buf_lens, nbufs, sizes, offset, &st2, &n2);
+    const int rc = gso_split_staged(st->ctx, read.data(), vlen, 0, bufs, buf_lens, nbufs, sizes, offset, &st2, &n2);
     if (rc) return rc;
     *n_out = n2;
     return st2;
