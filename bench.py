@@ -90,6 +90,10 @@ def parse():
     ap.add_argument("--poll", action="store_true",
                     help="poll the closing event before torch.cuda.synchronize() (slower: profiles/r4_probe_poll_ab.jsonl)")
     ap.add_argument("--no-affinity", action="store_true", help="do not bind each rank to its GPU's NUMA-local CPUs")
+    ap.add_argument("--warm-ms", type=float, default=40.0,
+                    help="configs[4] legs (cfg5_strong, --config cfg5): keep issuing warmup steps for at least this "
+                         "much wall time after the W contract steps (the chip streams ~15 %% slower for ~25 ms after "
+                         "idling; profiles/r5_cfg5_regions.jsonl); 0 = W steps only")
     ap.add_argument("--repeat", type=int, default=1,
                     help="diagnostics: time the K-step region this many times; `value` stays the FIRST region, "
                          "the others are listed under timing.repeats")
@@ -222,7 +226,7 @@ def main():
     use_events = not args.no_event_timing
     leg = checksum_leg(torch, dev, arena_np, pkts_np, mode, args.steps, args.warmup, args.streams, args.rotate,
                        barrier, use_events, repeat=args.repeat, verify=args.verify, gate=not args.no_gate,
-                       poll=args.poll)
+                       poll=args.poll, warm_ms=args.warm_ms if scaling == "strong" else 0.0)
     local_elapsed, kern_ms, iso_ms, S, R = leg["elapsed"], leg["kern_ms"], leg["iso_ms"], leg["streams"], leg["R"]
     elapsed = shard.max_over_ranks(local_elapsed, dist, device=red_dev)
     kern_all = shard.gather_floats(kern_ms if kern_ms is not None else -1.0, dist, device=red_dev)
@@ -285,6 +289,9 @@ def main():
                 "wall_us": round(uw * 1e6, 2), "GiB_per_s": round(bytes_per_step * args.steps / uw / 2**30, 2)}
             if um is not None:
                 result["timing"]["ungated"]["event_span_us"] = round(um * args.steps * 1e3, 2)
+        if leg.get("prewarm"):
+            result["timing"]["prewarm"] = {"warm_ms": args.warm_ms, "launches": leg["prewarm"],
+                                           "what": "untimed warmup launches beyond the W contract steps (--warm-ms)"}
         if leg["repeats"]:
             result["timing"]["repeats"] = [{"wall_us": round(w * 1e6, 1), "event_span_us": round(m * args.steps * 1e3, 1)}
                                            for w, m in leg["repeats"]]
@@ -397,7 +404,7 @@ def roofline(kname, bytes_per_step, flen, n, kern_ms, S, iso_ms, kern_all=None) 
 
 
 def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, rotate, barrier, use_events,
-                 repeat=1, verify=False, iso=True, gate=True, poll=False):
+                 repeat=1, verify=False, iso=True, gate=True, poll=False, warm_ms=0.0):
     """Time `steps` checksum launches (one batch each, inputs resident in HBM)
     after `warmup` untimed ones.  Returns {elapsed (this rank's wall s),
     kern_ms (HIP events, GPU ms per launch), iso_ms (one-stream reference),
@@ -491,6 +498,21 @@ def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, ro
         dev.checksum_batches(mode, batches(warmup, 0), strm, e0 if use_events else None,
                              e1 if use_events else None)
     torch.cuda.synchronize()
+    # Large launches (configs[4]: 1.57 GB each at N = 1) run ~15 % slower for
+    # the first ~25 ms of sustained streaming after the GPU sat idle (the
+    # process builds the 1 M-frame batch on the CPU first): the same 20-step
+    # region timed 4 times in a row reads 267 / 258 / 238 / 227 us per launch
+    # (profiles/r5_cfg5_regions.jsonl).  Such legs keep issuing warmup steps,
+    # in the same enqueue shape, for at least warm_ms of wall time beyond the
+    # W contract steps; the timed region is still exactly K steps.
+    prewarm = 0
+    if warm_ms > 0:
+        t_end = time.perf_counter() + warm_ms / 1e3
+        while time.perf_counter() < t_end:
+            dev.checksum_batches(mode, batches(8, warmup + prewarm), strm)
+            torch.cuda.synchronize()
+            prewarm += 8
+        warmup += prewarm
     if verify:
         if mode == MODE_VALIDATE:
             assert bool(outs[0][:n].all().item()), "VALIDATE: synthetic frames must all be valid"
@@ -513,7 +535,7 @@ def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, ro
         _, iso_ms = timed(max(steps, 20), warmup + steps, 1)
     del arenas, outs, pkts
     return {"elapsed": local_elapsed, "kern_ms": kern_ms, "iso_ms": iso_ms, "repeats": repeats, "streams": S, "R": R,
-            "ungated": ungated}
+            "ungated": ungated, "prewarm": prewarm}
 
 
 def strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_events) -> dict:
@@ -531,7 +553,7 @@ def strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_
     bytes_rank = int(pkts_np["len"].astype(np.int64).sum())
     S = 2
     leg = checksum_leg(torch, dev, arena_np, pkts_np, mode, args.steps, args.warmup, S, 2, barrier, use_events,
-                       iso=False, gate=not args.no_gate, poll=args.poll)
+                       iso=False, gate=not args.no_gate, poll=args.poll, warm_ms=args.warm_ms)
     del arena_np
     elapsed = shard.max_over_ranks(leg["elapsed"], dist, device=red_dev)
     kern_all = shard.gather_floats(leg["kern_ms"] if leg["kern_ms"] is not None else -1.0, dist, device=red_dev)
@@ -548,6 +570,8 @@ def strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_
         "packets_per_rank": [int(x) for x in ranges],
         "streams": leg["streams"],
         "rotated_copies": leg["R"],
+        "prewarm": {"warm_ms": args.warm_ms, "launches": leg["prewarm"],
+                    "what": "untimed warmup launches beyond the W contract steps (--warm-ms)"},
     }
     if leg["kern_ms"] is not None:
         out["roofline"] = roofline(kernel_name(mode), bytes_rank, flen, hi - lo, leg["kern_ms"], leg["streams"], None,

@@ -22,11 +22,14 @@ L.probe_launch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ct
 L.probe_glds_launch.argtypes = L.probe_launch.argtypes
 outs = [torch.empty(65536 * 256, dtype=torch.int32, device="cuda") for _ in range(2)]
 sts = [torch.cuda.Stream(), torch.cuda.Stream()]
-for nbytes, R, K in ((98304000, 4, 200), (1572864000, 2, 20)):
+SIZES = ((98304000, 4, 200), (1572864000, 2, 20))
+if os.environ.get("BIG_ONLY"):
+    SIZES = SIZES[1:]
+for nbytes, R, K in SIZES:
     bufs = [torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda") for _ in range(R)]
     for ns in (1, 2):
         for kind, grid, u in (("reg", 2048, 4), ("reg", 4096, 4), ("reg", 8192, 4), ("reg", 4096, 8),
-                              ("reg", 16384, 4), ("glds", 2048, 4), ("glds", 4096, 4)):
+                              ("reg", 16384, 4), ("glds", 2048, 4), ("glds", 4096, 4))[:int(os.environ.get("NSHAPES", "7"))]:
             fn = L.probe_launch if kind == "reg" else L.probe_glds_launch
 
             def run(K):
@@ -47,9 +50,15 @@ for nbytes, R, K in ((98304000, 4, 200), (1572864000, 2, 20)):
                 return e0.elapsed_time(e1) * 1e3 / K
 
             run(4)
+            warm_ms = float(os.environ.get("WARM_MS", "0"))  # sustained launches before timing (r5_cfg5_regions)
+            if warm_ms > 0:
+                import time
+                t_end = time.perf_counter() + warm_ms / 1e3
+                while time.perf_counter() < t_end:
+                    run(8)
             us = min(run(K) for _ in range(3))
             print(json.dumps({"bytes": nbytes, "kind": kind, "streams": ns, "grid": grid, "U": u, "nt": 1,
-                              "us_per_launch": round(us, 2), "frac_of_8TBps": round(nbytes / us / 1e3 / 8000, 4)}),
+                              "warm_ms": float(os.environ.get("WARM_MS", "0")), "us_per_launch": round(us, 2), "frac_of_8TBps": round(nbytes / us / 1e3 / 8000, 4)}),
                   flush=True)
     del bufs
     torch.cuda.empty_cache()
