@@ -42,9 +42,10 @@ def bench_key(k):
     if m:
         mode = {"2": "VALIDATE", "1": "L4_FILL"}.get(m.group(1), m.group(1))
         return f"checksum_batch_kernel<{mode},{m.group(2)},{m.group(3)},{'nt' if m.group(4) == 'true' else 'rt'}>"
-    m = re.search(r"gso_lds_kernel<(\d+), (\d+), (true|false)>", k)
-    if m:
-        return f"gso_lds_kernel<{m.group(1)},{m.group(2)},{m.group(3)}>"
+    m = re.search(r"gso_lds_kernel<(\d+), (\d+), (true|false)(?:, (\d+))?>", k)
+    if m:  # round 5 added a fourth argument, parts per job (1: named as before)
+        p = m.group(4) if m.group(4) and m.group(4) != "1" else None
+        return f"gso_lds_kernel<{m.group(1)},{m.group(2)},{m.group(3)}" + (f",{p}>" if p else ">")
     m = re.search(r"gso_rows_kernel<(\d+), (true|false)(?:, (\d+))?>", k)
     if m:  # round 1 / early round 2 had a third template argument (block waves)
         return f"gso_rows_kernel<{m.group(1)},{m.group(2)}" + (f",{m.group(3)}>" if m.group(3) else ">")

@@ -24,7 +24,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-SO = os.path.join(ROOT, "scripts", "probe_so", "libwgcsum_gso_stamps.so")
+SO = os.environ.get("STAMPS_SO") or os.path.join(ROOT, "scripts", "probe_so", "libwgcsum_gso_stamps.so")
 
 if len(sys.argv) > 1 and sys.argv[1] == "build":
     from wireguard_amd import build as B

@@ -1289,10 +1289,20 @@ struct LdsHead {
   int32_t clean;  // 1: the row-streaming path (a clean job, gso_rows_kernel's criterion)
   int32_t type, ipv, hdr_len, gso, cs, co, plen;
   uint32_t ip_base, l4_base, tflags, id0, seq0;
+  uint4 q[16];  // readBuf[16r, 16r + 16) per row lane r (P > 1 with WGCS_GSO_QLDS)
 };
 
 #ifndef WGCS_GSO_LDS_WAVES
 #define WGCS_GSO_LDS_WAVES 8
+#endif
+#ifndef WGCS_GSO_PARTS
+#define WGCS_GSO_PARTS 1  // r5: P = 3 x 4 waves is 4-9 % faster on four streams, 11 % slower on one (r5_gso_parts*)
+#endif
+#ifndef WGCS_GSO_QLDS
+#define WGCS_GSO_QLDS 1  // P > 1: wave 0 publishes the header chunks through LDS (0: every wave loads them)
+#endif
+#ifndef WGCS_GSO_PART_XCD
+#define WGCS_GSO_PART_XCD 1  // P > 1: a job's parts on one XCD (0: consecutive blocks)
 #endif
 // One workgroup of NW waves per job.  Wave 0 issues the header loads, then
 // every wave its share of the LDS-DMA loads of the whole job; wave 0 runs the
@@ -1302,17 +1312,30 @@ struct LdsHead {
 // with write-through full-chunk stores: the segment stores follow the loads in
 // this kernel, so the lines go to HBM while the rows still work instead of
 // in one end-of-kernel writeback of every segment (≈ 17 MB for cfg4).
-template <int NW, int U, bool NT>
+// P > 1 (round 5): P workgroups per job, each staging about 1/P of the job
+// (part p: the segments whose payload starts in job bytes [p H, (p + 1) H),
+// H = len / P rounded up to 16, plus one segment's worth past that for the
+// last one), so a block holds 1/P of the LDS and rows -- P = 2: 40 KB, 4
+// blocks per CU instead of 2 -- and its rows run one pass.  The parts of a job
+// are dealt to one XCD (their shared header lines and boundary bytes meet in
+// one L2).  Every part runs the head; part 0 writes count / status and runs
+// the decoded path of a job that is not clean.  A row whose bytes lie outside
+// its part's image (gsoSize > 1,536) streams from HBM.
+template <int NW, int U, bool NT, int P>
 __global__ __launch_bounds__(NW * 64) void gso_lds_kernel(const uint8_t* __restrict__ arena,
                                                            const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
                                                            uint8_t* __restrict__ out, uint32_t out_stride,
                                                            const GsoOutPos* __restrict__ outpos, uint32_t offset,
                                                            uint32_t room, int32_t* __restrict__ sizes,
-                                                           int32_t* __restrict__ count, int32_t* __restrict__ status) {
-  constexpr int ROWS = NW * 4;                                        // 16-lane rows per workgroup
-  constexpr int kIters = (kImgBytes / 16 + NW * 64 - 1) / (NW * 64);  // LDS-DMA instructions per wave
-  constexpr int kArr = kIters * NW * 64 * 16;                         // every slot a DMA writes
-  static_assert(kArr >= kImgBytes + 1552, "image slack for the windows past a job's end");
+                                                           int32_t* __restrict__ count, int32_t* __restrict__ status, uint32_t n_jobs) {
+  constexpr int ROWS = NW * 4;  // 16-lane rows per workgroup
+  // a part's staged bytes: H (at most kImgBytes / P rounded up) + 48 before +
+  // kPartTail past its end; the image also holds 1,552 bytes of window slack
+  constexpr int kPartTail = 1536 + 32;
+  constexpr int kStage = P == 1 ? kImgBytes : ((kImgBytes + P - 1) / P + 15) / 16 * 16 + 48 + kPartTail + 16;
+  constexpr int kIters = ((kStage + 1552) / 16 + NW * 64 - 1) / (NW * 64);  // LDS-DMA instructions per wave
+  constexpr int kArr = kIters * NW * 64 * 16;                      // every slot a DMA writes
+  static_assert(kArr >= kStage + 1552, "image slack for the windows past a job's end");
   __shared__ __attribute__((aligned(16))) uint8_t img[kArr];
   __shared__ LdsHead hd;
 #ifdef WGCS_GSO_STAMPS  // timing-only build (scripts/probe_gso_stamps.py, LDS kernel: NWAVES=NW)
@@ -1321,7 +1344,19 @@ __global__ __launch_bounds__(NW * 64) void gso_lds_kernel(const uint8_t* __restr
   const int lane = threadIdx.x & 63;
   const int r = lane & 15;
   const int wv = threadIdx.x >> 6;
-  const uint32_t jb = blockIdx.x;
+  uint32_t jb = blockIdx.x;
+  int part = 0;
+  if (P > 1) {  // blocks b, b + 8, ... share an XCD: job (k / P) * 8 + b % 8, part k % P (k = b / 8)
+    if (WGCS_GSO_PART_XCD) {
+      const uint32_t k = blockIdx.x >> 3;
+      jb = (k / P) * 8 + (blockIdx.x & 7u);
+      part = (int)(k % P);
+    } else {
+      jb = blockIdx.x / P;
+      part = (int)(blockIdx.x % P);
+    }
+    if (jb >= n_jobs) return;  // the grid is padded to a multiple of 8 jobs
+  }
   const wgcs_gso_job job = jobs[jb];
   const uint8_t* vb = arena + job.off;
   const uint32_t jlen = job.len;
@@ -1337,7 +1372,18 @@ __global__ __launch_bounds__(NW * 64) void gso_lds_kernel(const uint8_t* __restr
   }
   const int ibias = (int)((uintptr_t)vb & 15u);
   const int nch = (int)((jlen + (uint32_t)ibias + 15u) >> 4);
-  const bool use_img = jlen >= 14 && nch <= kImgBytes / 16;  // block-uniform
+  // this part's image: chunks [q_lo, q_lo + q_n) of the job (chunk q = the
+  // aligned 16 bytes at (vb & ~15) + 16 q); job byte x at image offset x + ib_p
+  const int H = P == 1 ? 0 : (int)(((jlen + P - 1) / P + 15u) & ~15u);
+  int q_lo = 0, q_n = nch;
+  if (P > 1) {
+    q_lo = max(0, (part * H + ibias) / 16 - 3);
+    const int q_hi = part == P - 1 ? nch : min(nch, ((part + 1) * H + kPartTail + ibias + 15) / 16);
+    q_n = max(0, q_hi - q_lo);
+  }
+  const int ib_p = ibias - 16 * q_lo;
+  const bool use_img = P == 1 ? (jlen >= 14 && nch <= kImgBytes / 16)  // block-uniform
+                              : (jlen >= 14 && q_n <= kStage / 16);
   const bool raw = (job.flags & WGCS_GSO_JOB_RAW) != 0;
   // ---- wave 0: header chunks (as gso_rows_kernel) and the virtio header +
   // readBuf[0] (16 bytes from the dword holding vb[0], range-checked: zeros
@@ -1349,6 +1395,7 @@ __global__ __launch_bounds__(NW * 64) void gso_lds_kernel(const uint8_t* __restr
       const_cast<uint8_t*>(hbase), (short)0, (int)(jlen + 3u) - (int)(hbase - vb), 0x00020000);
   const int sh = (int)((uintptr_t)vb & 3u);
   uint4 H0 = make_uint4(0, 0, 0, 0), w = make_uint4(0, 0, 0, 0);
+  if (P > 1 && !WGCS_GSO_QLDS && wv != 0) H0 = bld16<false>(hrs, 16 * r);  // the header chunks (Q) of every row
   if (wv == 0) {
     H0 = bld16<false>(hrs, 16 * r);
     const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
@@ -1365,7 +1412,7 @@ __global__ __launch_bounds__(NW * 64) void gso_lds_kernel(const uint8_t* __restr
   // loads behind wave 0's header loads.
   {
     const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(vb - ibias), (short)0, use_img ? 16 * nch : 0, 0x00020000);
+        const_cast<uint8_t*>(vb - ibias + 16 * q_lo), (short)0, use_img ? 16 * q_n : 0, 0x00020000);
 #pragma unroll
     for (int it = 0; it < kIters; ++it) {
       const int q0 = (it * NW + wv) * 64;  // this wave-instruction's first chunk (1 KiB of LDS)
@@ -1420,7 +1467,7 @@ __global__ __launch_bounds__(NW * 64) void gso_lds_kernel(const uint8_t* __restr
     }
     uint32_t ip_base = 0, l4_base = 0, tflags = 0, id0 = 0, seq0 = 0;
     if (ufl(clean ? 1 : 0)) {
-      if (lane == 0) {  // the checks can only end in the segment count here (gso_rows_kernel)
+      if (lane == 0 && part == 0) {  // the checks can only end in the segment count here (gso_rows_kernel)
         const int nfull_s = (plen_s - hdr_s + gso_s - 1) / gso_s;
         const bool many = nfull_s > (int)max_segs;
         count[jb] = many ? (int)max_segs - 1 : nfull_s;
@@ -1466,6 +1513,9 @@ __global__ __launch_bounds__(NW * 64) void gso_lds_kernel(const uint8_t* __restr
       hd.id0 = id0;
       hd.seq0 = seq0;
     }
+    if (P > 1 && WGCS_GSO_QLDS) {  // the head's Q (every row of wave 0 holds it; row 0 publishes)
+      if (lane < 16) hd.q[lane] = Q;
+    }
   }
 #ifdef WGCS_GSO_STAMPS
   stp[1] = __builtin_amdgcn_s_memrealtime();
@@ -1490,7 +1540,13 @@ __global__ __launch_bounds__(NW * 64) void gso_lds_kernel(const uint8_t* __restr
     // readBuf[16r, 16r + 16): from the image, or (a job too large for it)
     // from HBM as gso_rows_kernel reads it
     uint4 Q;
-    if (use_img) {
+    if (P > 1 && WGCS_GSO_QLDS) {  // published by wave 0
+      Q = hd.q[r];
+    } else if (P > 1) {  // from the header loads every wave issued first
+      const uint32_t nx = row_next(H0.x);
+      Q = make_uint4(__builtin_amdgcn_alignbyte(H0.y, H0.x, hph), __builtin_amdgcn_alignbyte(H0.z, H0.y, hph),
+                     __builtin_amdgcn_alignbyte(H0.w, H0.z, hph), __builtin_amdgcn_alignbyte(nx, H0.w, hph));
+    } else if (use_img) {
       const int dq = ibias + 10 + 16 * r, s = dq & 3;
       const uint4 T = img16(img, dq - s);
       const uint32_t T4 = img4(img, dq - s + 16);
@@ -1509,18 +1565,33 @@ __global__ __launch_bounds__(NW * 64) void gso_lds_kernel(const uint8_t* __restr
     const bool wt = WGCS_GSO_WT && (uint64_t)max_segs * opitch + offset < 0x7FFF0000ull;
     uint8_t* const obase16 = out + obase - ((uintptr_t)(out + obase) & 15u);
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(obase16, (short)0, 0x7FFFFFFF, 0x00020000);
-    for (int i = wv * 4 + (lane >> 4); has_seg(i); i += ROWS) {  // row-uniform
+    // this part's segments: payload start (job byte 10 + hdrLen + i gso) in
+    // [part H, (part + 1) H)
+    int i0 = 0, i1 = 0x7FFFFFFF;
+    if (P > 1) {
+      const int64_t a = (int64_t)part * H - 10 - hdr_len, b = a + H;
+      i0 = a <= 0 ? 0 : (int)min((a + gso - 1) / gso, (int64_t)0x7FFFFFFF);
+      if (part < P - 1) i1 = b <= 0 ? 0 : (int)min((b + gso - 1) / gso, (int64_t)0x7FFFFFFF);
+    }
+    const int lo_b = 16 * q_lo - ibias, hi_b = 16 * (q_lo + q_n) - ibias;  // staged job bytes
+    for (int i = i0 + wv * 4 + (lane >> 4); i < i1 && has_seg(i); i += ROWS) {  // row-uniform
       uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
       const int dalign = (int)((uintptr_t)dst & 15u);
       uint8_t* dbase = dst - dalign;
       uint32_t acc = 0;
-      if (use_img) {
+      bool in_img = use_img;
+      if (P > 1 && in_img) {  // the row's payload windows staged, and every window it reads inside the image
+        const RowSrc g = row_src(rb, i, gso, hdr_len, plen, dalign);
+        in_img = g.lo - 18 >= lo_b && (g.hi + 20 <= hi_b || q_lo + q_n >= nch) &&
+                 ib_p + g.aoff + 16 * ((g.nk + 16 * U - 1) / (16 * U) * 16 * U) + 4 <= kArr;
+      }
+      if (in_img) {
         RowOut ro;
         ro.keep = make_uint4(0, 0, 0, 0);
         ro.rs = ors;
         ro.dro = (int)(dbase - obase16);
         ro.wt = wt;
-        stream_row_img<U>(img, ibias, rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, ro);
+        stream_row_img<U>(img, ib_p, rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, ro);
         finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
                    tflags, id0, seq0, &sizes[slot0 + (uint32_t)i], &ro);
       } else {
@@ -1533,12 +1604,12 @@ __global__ __launch_bounds__(NW * 64) void gso_lds_kernel(const uint8_t* __restr
     stp[3] = __builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stp[4] = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0 && max_segs >= 128 && wv < 12) {
-      int32_t* sp = sizes + slot0 + 64 + wv * 5;
+    if (lane == 0 && max_segs >= 128 && part * NW + wv < 12) {
+      int32_t* sp = sizes + slot0 + 64 + (part * NW + wv) * 5;
       for (int k = 0; k < 5; ++k) sp[k] = (int32_t)(uint32_t)stp[k];
     }
 #endif
-  } else {
+  } else if (part == 0) {
     // every other job: the decoded path, NW * 4 rows per group (the image's
     // loads have drained above, so no LDS-DMA write can land after the
     // workgroup retires)
@@ -1566,8 +1637,15 @@ hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs
   }();
   if (!use_rows) {
     constexpr int NW = WGCS_GSO_LDS_WAVES;
-    hipLaunchKernelGGL((gso_lds_kernel<NW, WGCS_GSO_U, true>), dim3(n_jobs), dim3(NW * 64), 0, s, arena, jobs,
-                       max_segs, out, out_stride, outpos, offset, room, sizes, count, status);
+    constexpr int P = WGCS_GSO_PARTS;
+    if (P == 1) {
+      hipLaunchKernelGGL((gso_lds_kernel<NW, WGCS_GSO_U, true, 1>), dim3(n_jobs), dim3(NW * 64), 0, s, arena, jobs,
+                         max_segs, out, out_stride, outpos, offset, room, sizes, count, status, n_jobs);
+    } else {  // (n_jobs rounded up to 8) x P blocks
+      if ((uint64_t)(n_jobs + 7u) / 8u * 8u * P > 0x7FFFFFFFull) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((gso_lds_kernel<NW, WGCS_GSO_U, true, P>), dim3((n_jobs + 7u) / 8u * 8u * P), dim3(NW * 64), 0,
+                         s, arena, jobs, max_segs, out, out_stride, outpos, offset, room, sizes, count, status, n_jobs);
+    }
     return hipGetLastError();
   }
   // 16 segments (4 waves) per block and group; a few blocks per job, each
