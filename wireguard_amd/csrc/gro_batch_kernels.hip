@@ -5,15 +5,16 @@
 // handleGRO (gro.go:1326-1367) is order-dependent inside one call (flow
 // table, sequence adjacency, prepend swaps) but calls are independent, so the
 // batch maps to one 256-thread block per call:
-//   1. every thread takes one buffer: slice header, handleGRO's offset check,
-//      groCandidate (gro.go:1280-1317), the tcpGRO / udpGRO pre-checks that end
-//      in groResultNoop, and the header fields the table needs (seq, gsoSize,
-//      PSH, the IP fields ipHeadersCanCoalesce compares);
+//   1. every thread takes one buffer: slice header, handleGRO's offset check;
+//      then one 16-lane DPP row per packet reads the packet once: groCandidate
+//      (gro.go:1280-1317), the tcpGRO / udpGRO pre-checks that end in
+//      groResultNoop, the header fields the table needs (seq, gsoSize, PSH,
+//      the IP fields ipHeadersCanCoalesce compares) from its first 64 bytes,
+//      and checksumValid (gro.go:554-612) of every candidate from all of them
+//      -- exact up front because the reference validates before it mutates
+//      (gro.go:665-681, :709-723, :767-775);
 //   2. flow ids: each packet finds the first earlier packet of its table with
 //      the same flow key (tcpFlowKey / udpFlowKey, gro.go:96-127, :252-275);
-//      checksumValid (gro.go:554-612) of every candidate, one 16-lane DPP row
-//      per packet -- exact up front because the reference validates before it
-//      mutates (gro.go:665-681, :709-723, :767-775);
 //   3. the loop of handleGRO over those precomputed fields, one thread per
 //      flow (flows never interact): tcpGRO / udpGRO with the flow's items as a
 //      linked list in LDS, coalesceTCPPackets / coalesceUDPPackets as piece
@@ -78,6 +79,7 @@ struct GroSmem {
   // long TCP flows walked by a whole wave (Planner::run_flow_wave): the flow's
   // packet count, its items as an array (fitem[fbase[f] .. fbase[f] + fnit[f])
   // in insertion order), the list of such flows
+  uint8_t hdr[16][80];    // step 1: each row's packet bytes 0..63 (its first five aligned chunks)
   uint32_t fsize[kMaxB];  // packets of the flow
   int16_t fbase[kMaxB], fnit[kMaxB], fitem[kMaxB], coop[kMaxB];
   int n_eff, n_write, n_mat, n_coop, fitem_top;
@@ -859,108 +861,139 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
     S.ndst[t] = kNone;
     S.fsize[t] = 0;
   }
-  // groCandidate + the tcpGRO / udpGRO checks that return groResultNoop
-  if (t < n_eff) {
-    const uint8_t* pk = arena + S.boff[t] + offset;
-    const uint32_t pl = S.blen[t] - (uint32_t)offset;
-    // Every field below lies in the first 64 packet bytes (IPv4 with IHL 5
-    // or IPv6, then the TCP / UDP header).  A packet of >= 80 bytes brings
-    // them in with one batch of five aligned 16-byte loads (all inside the
-    // packet), shifted to packet coordinates: one memory round trip instead
-    // of a chain of dependent byte loads.  A shorter one reads byte by byte.
-    const bool win = pl >= 80;
-    uint4 P0 = make_uint4(0, 0, 0, 0), P1 = P0, P2 = P0, P3 = P0;
-    if (win) {
-      const uint8_t* a0 = reinterpret_cast<const uint8_t*>((uintptr_t)pk & ~(uintptr_t)15);
-      const int sh = (int)((uintptr_t)pk & 15u);
-      const uint4 c0 = ld16(a0), c1 = ld16(a0 + 16), c2 = ld16(a0 + 32), c3 = ld16(a0 + 48), c4 = ld16(a0 + 64);
-      P0 = funnel(c0, c1, sh);
-      P1 = funnel(c1, c2, sh);
-      P2 = funnel(c2, c3, sh);
-      P3 = funnel(c3, c4, sh);
+  // groCandidate + the tcpGRO / udpGRO checks that return groResultNoop, and
+  // checksumValid of every candidate, in one pass over each packet (round
+  // 5): one 16-lane row per packet loads its aligned 16-byte chunks once (6
+  // per lane in flight, 1,536 bytes); the header fields come from the first
+  // five chunks (packet bytes 0..63, fetched across the row), the L4 checksum
+  // (gro.go:554-612) from all of them.  Until round 4 a thread per packet read
+  // the header with its own five loads and a row read the packet again after
+  // the flow ids: the packet's first 128-byte line came from HBM twice.
+  __syncthreads();  // the slot state above, before the rows write packet fields
+  for (int p = row; p < n_eff; p += 16) {  // row-uniform
+    constexpr int U = 6;
+    const uint8_t* pk = arena + S.boff[p] + offset;
+    const int pl = (int)(S.blen[p] - (uint32_t)offset);
+    const uint8_t* a0 = reinterpret_cast<const uint8_t*>((uintptr_t)pk & ~(uintptr_t)15);
+    const int sh = (int)((uintptr_t)pk & 15u);
+    const int nch = (pl + sh + 15) >> 4;
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = r + 16 * u;
+      v[u] = c < nch ? ld16(a0 + 16 * c) : make_uint4(0, 0, 0, 0);
     }
-    // byte k (< 64, a compile-time constant after unrolling) of the packet
-    auto B = [&](int k) -> uint32_t {
-      if (!win) return pk[k];
-      const uint4& q = k < 16 ? P0 : (k < 32 ? P1 : (k < 48 ? P2 : P3));
-      const int d = (k >> 2) & 3;
-      const uint32_t w = d == 0 ? q.x : (d == 1 ? q.y : (d == 2 ? q.z : q.w));
-      return (w >> (8 * (k & 3))) & 0xFFu;
-    };
+    // packet bytes 0..63: chunks 0..4 (the row's lanes 0..4) staged in the
+    // row's LDS slot, read back byte by byte (broadcast reads; registers
+    // holding them would spill at this kernel's 72-VGPR budget)
+    wave_lds_sync();  // the row's reads of its previous packet's bytes come first
+    if (r < 5) *reinterpret_cast<uint4*>(&S.hdr[row][16 * r]) = v[0];
+    wave_lds_sync();
+    const uint8_t* hb = &S.hdr[row][sh];
+    // byte k (< 64) of the packet; every byte the checks below read lies
+    // below len(pkt) (each read is behind its length check), and every such
+    // byte is in a loaded chunk
+    auto B = [&](int k) -> uint32_t { return hb[k]; };
     auto BE16 = [&](int k) -> uint32_t { return (B(k) << 8) | B(k + 1); };
     auto BE32 = [&](int k) -> uint32_t { return (BE16(k) << 16) | BE16(k + 2); };
+    // checksumValid's sum first, so the chunks die before the header checks:
+    // pkt[iphLen:] with iphLen from the version nibble (every candidate's; a
+    // packet that is none never uses it), chunk c at L4 position 16 c - sh -
+    // iphLen, more batches for a packet past 1,536 bytes
+    const int ihv = (B(0) >> 4) == 6 ? 40 : 20;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += chunk_sum(v[u], 16 * (r + 16 * u) - sh - ihv, 0, pl - ihv);
     uint8_t c = C_NOT;
     if (pl >= 28) {  // gro.go:1280-1317
-      const uint32_t b0 = B(0), v = b0 >> 4;
-      if (v == 4 && (b0 & 0x0F) == 5) {
+      const uint32_t b0 = B(0), ver = b0 >> 4;
+      if (ver == 4 && (b0 & 0x0F) == 5) {
         const uint32_t pr = B(9);
         if (pr == 6 && pl >= 40) c = C_TCP4;
         else if (pr == 17 && can_udp) c = C_UDP4;
-      } else if (v == 6) {
+      } else if (ver == 6) {
         const uint32_t nh = B(6);
         if (nh == 6 && pl >= 60) c = C_TCP6;
         else if (nh == 17 && pl >= 48 && can_udp) c = C_UDP6;
       }
     }
-    S.cand[t] = c;
-    if (c != C_NOT) {
+    if (r == 0) S.cand[p] = c;
+    if (c != C_NOT) {  // row-uniform
       const bool v6 = c == C_TCP6 || c == C_UDP6, tcp = c <= C_TCP6;
       const int ih = v6 ? 40 : 20;  // IPv4 candidates have IHL 5
       bool nop = pl > 65535;
-      if (v6) nop = nop || BE16(4) != pl - 40;
-      else nop = nop || BE16(2) != pl;
+      if (v6) nop = nop || BE16(4) != (uint32_t)(pl - 40);
+      else nop = nop || BE16(2) != (uint32_t)pl;
       int thl = 8;
       uint32_t fl = 0;
       if (tcp) {
-        nop = nop || pl < (uint32_t)ih;
+        nop = nop || pl < ih;
         thl = (int)((v6 ? B(52) : B(32)) >> 4) * 4;
-        nop = nop || thl < 20 || thl > 60 || pl < (uint32_t)(ih + thl);
+        nop = nop || thl < 20 || thl > 60 || pl < ih + thl;
       } else {
-        nop = nop || pl < (uint32_t)(ih + 8);
+        nop = nop || pl < ih + 8;
       }
       if (!v6) nop = nop || (B(6) & 0x20) || (uint8_t)(B(6) << 3) || B(7);  // fragments
       if (!nop && tcp) {
         fl = v6 ? B(53) : B(33);
         nop = fl != 0x10 && fl != 0x18;  // ACK, or ACK|PSH
       }
-      const int g = nop ? 0 : (int)pl - ih - thl;
+      const int g = nop ? 0 : pl - ih - thl;
       nop = nop || g < 1;
-      S.noop[t] = nop ? 1 : 0;
-      S.iph[t] = (uint8_t)ih;
-      S.th[t] = (uint8_t)thl;
-      S.psh[t] = (fl & 0x08) ? 1 : 0;
-      S.gso[t] = (uint16_t)g;
-      if (!nop) {
-        S.seq[t] = tcp ? (v6 ? BE32(44) : BE32(24)) : 0u;
-        S.ipattr[t] = v6 ? B(0) | ((B(1) >> 4) << 8) | (B(7) << 16) | (6u << 24)
-                         : B(1) | ((B(6) >> 5) << 8) | (B(8) << 16) | (4u << 24);
-        // flow key words (addresses, ports, ack for TCP) into LDS + their hash
-        uint32_t h = 2166136261u;
-        if (v6) {
+      if (r == 0) {
+        S.noop[p] = nop ? 1 : 0;
+        S.iph[p] = (uint8_t)ih;
+        S.th[p] = (uint8_t)thl;
+        S.psh[p] = (fl & 0x08) ? 1 : 0;
+        S.gso[p] = (uint16_t)g;
+      }
+      if (!nop) {  // row-uniform
+        if (r == 0) {
+          S.seq[p] = tcp ? (v6 ? BE32(44) : BE32(24)) : 0u;
+          S.ipattr[p] = v6 ? B(0) | ((B(1) >> 4) << 8) | (B(7) << 16) | (6u << 24)
+                           : B(1) | ((B(6) >> 5) << 8) | (B(8) << 16) | (4u << 24);
+          // flow key words (addresses, ports, ack for TCP) into LDS + their hash
+          uint32_t h = 2166136261u;
+          if (v6) {
 #pragma unroll
-          for (int w = 0; w < 8; ++w) {
-            const uint32_t x = BE32(8 + 4 * w);
-            S.kw[t][w] = x;
-            h = fnv(h, x);
-          }
-        } else {
+            for (int w = 0; w < 8; ++w) {
+              const uint32_t x = BE32(8 + 4 * w);
+              S.kw[p][w] = x;
+              h = fnv(h, x);
+            }
+          } else {
 #pragma unroll
-          for (int w = 0; w < 2; ++w) {
-            const uint32_t x = BE32(12 + 4 * w);
-            S.kw[t][w] = x;
-            h = fnv(h, x);
+            for (int w = 0; w < 2; ++w) {
+              const uint32_t x = BE32(12 + 4 * w);
+              S.kw[p][w] = x;
+              h = fnv(h, x);
+            }
           }
+          const int nab = v6 ? 32 : 8;
+          const uint32_t ports = v6 ? BE32(40) : BE32(20);
+          const uint32_t ack = tcp ? (v6 ? BE32(48) : BE32(28)) : 0u;
+          S.kw[p][nab / 4] = ports;
+          S.kw[p][nab / 4 + 1] = ack;
+          S.keyh[p] = fnv(fnv(fnv(h, ports), ack), c);
+          uint32_t oh = 2166136261u;
+          if (tcp)
+            for (int k = 20; k < thl; ++k) oh = fnv(oh, pk[ih + k]);
+          S.opth[p] = oh;
         }
-        const int nab = v6 ? 32 : 8;
-        const uint32_t ports = v6 ? BE32(40) : BE32(20);
-        const uint32_t ack = tcp ? (v6 ? BE32(48) : BE32(28)) : 0u;
-        S.kw[t][nab / 4] = ports;
-        S.kw[t][nab / 4 + 1] = ack;
-        S.keyh[t] = fnv(fnv(fnv(h, ports), ack), c);
-        uint32_t oh = 2166136261u;
-        if (tcp)
-          for (int k = 20; k < thl; ++k) oh = fnv(oh, pk[ih + k]);
-        S.opth[t] = oh;
+        // checksumValid's fold (ih == ihv for every candidate)
+        uint32_t sm = fold32_16(row16_sum_u32(fold64_16(acc)));
+        if (((uintptr_t)(pk + ih) & 1u) == 0) sm = bswap16(sm);  // LE pairs at even addresses -> BE words from L4
+        // pseudo header: addresses (BE words), protocol, L4 length (gro.go:561-571);
+        // lane r's word at packet byte 8 + 2r (IPv6: 16 words from 8; IPv4: lanes 2..5, bytes 12..19)
+        const int ka = 8 + 2 * r;
+        const bool in_a = v6 ? r < 16 : (r >= 2 && r < 6);
+        const uint32_t aw = in_a ? ((uint32_t)hb[ka] << 8) | hb[ka + 1] : 0u;
+        const uint32_t ad = row16_sum_u32(aw);
+        const uint32_t tt = fold32_16(sm + fold32_16(ad) + (tcp ? 6u : 17u) + (uint32_t)((pl - ih) & 0xFFFF));
+        // a packet past 1,536 bytes (not an MTU-sized Write) is summed
+        // whole after the flow ids (row_checksum_valid: a second batch in
+        // this loop would cost the kernel ~40 spilled VGPRs); 2 = pending
+        if (r == 0) S.valid[p] = nch > 16 * U ? 2 : (tt == 0xFFFFu ? 1 : 0);
       }
     }
   }
@@ -1001,13 +1034,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
     }
     S.fnext[t] = (int16_t)nx;
   }
-  // checksumValid of every candidate: one 16-lane row per packet
+  // checksumValid of the candidates past 1,536 bytes (step 1 left them pending)
   for (int p = row; p < n_eff; p += 16) {  // row-uniform
-    if (S.cand[p] == C_NOT || S.noop[p]) continue;
+    if (S.valid[p] != 2) continue;
     const uint8_t c = S.cand[p];
     const bool v6 = c == C_TCP6 || c == C_UDP6;
     const bool ok = row_checksum_valid(arena + S.boff[p] + offset, (int)(S.blen[p] - offset), S.iph[p], v6,
                                        c <= C_TCP6 ? 6u : 17u, r);
+    wave_lds_sync();  // every lane of the row has read S.valid[p]
     if (r == 0) S.valid[p] = ok ? 1 : 0;
   }
   __syncthreads();
