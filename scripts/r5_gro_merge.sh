@@ -30,7 +30,7 @@ for l in open(sys.argv[1]):
     print(f"{d['shape']:10s} {d['lib']:24s} {d['round']} {d['value']/1e6:8.1f} M/s kern {r['kernel_ms']*1e3:7.1f} us frac {r['frac']:.4f}")
 PY
 SIZED="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_32B_sum"
-for shape in ${PMC_SHAPES:-4x32 shuffled}; do
+for shape in ${PMC_SHAPES-4x32 shuffled}; do
   for lib in $LIBS; do
     p=$ROOT/$lib; [ "$lib" = libwgcsum.so ] && p=$ROOT/wireguard_amd/libwgcsum.so
     name=$(basename $lib .so)
