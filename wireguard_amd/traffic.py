@@ -1,8 +1,11 @@
 """Per-launch HBM traffic of the path's kernels, as the bench lines report it
 (roofline.traffic): read from the committed profiles/traffic.json, which
-scripts/pmc_traffic.py writes from separate rocprofv3 FETCH_SIZE / WRITE_SIZE
-passes (FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024 on gfx950,
-MI355X_MICROARCH.md §HBM).  Bench-side bookkeeping only, not the data path."""
+scripts/pmc_traffic.py writes from separate rocprofv3 passes.  Round-5
+records: reads from the L2's sized read requests (128 x TCC_EA0_RDREQ_128B +
+64 x _64B + 32 x _32B, scripts/pmc_sized.py) + WRITE_SIZE x 1024, with the
+guide's FETCH_SIZE x 1024 x 2 beside them (read_bytes_fetch_x2; within 1 %
+for every kernel, profiles/r5_pmc/).  Bench-side bookkeeping only, not the
+data path."""
 from __future__ import annotations
 
 import json
