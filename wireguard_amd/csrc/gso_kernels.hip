@@ -1322,7 +1322,12 @@ struct LdsHead {
 // the decoded path of a job that is not clean.  A row whose bytes lie outside
 // its part's image (gsoSize > 1,536) streams from HBM.
 template <int NW, int U, bool NT, int P>
-__global__ __launch_bounds__(NW * 64) void gso_lds_kernel(const uint8_t* __restrict__ arena,
+#ifdef WGCS_GSO_LDS_WPE  // A/B builds: waves per SIMD to compile for (VGPR budget)
+#define WGCS_GSO_LDS_ATTR __attribute__((amdgpu_waves_per_eu(WGCS_GSO_LDS_WPE, 8)))
+#else
+#define WGCS_GSO_LDS_ATTR
+#endif
+__global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(const uint8_t* __restrict__ arena,
                                                            const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
                                                            uint8_t* __restrict__ out, uint32_t out_stride,
                                                            const GsoOutPos* __restrict__ outpos, uint32_t offset,
