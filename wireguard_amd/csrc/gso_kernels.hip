@@ -1301,6 +1301,9 @@ struct LdsHead {
 #ifndef WGCS_GSO_QLDS
 #define WGCS_GSO_QLDS 1  // P > 1: wave 0 publishes the header chunks through LDS (0: every wave loads them)
 #endif
+#ifndef WGCS_GSO_SHEAD
+#define WGCS_GSO_SHEAD 1  // P > 1: the head's loads through the scalar path
+#endif
 #ifndef WGCS_GSO_PART_XCD
 #define WGCS_GSO_PART_XCD 1  // P > 1: a job's parts on one XCD (0: consecutive blocks)
 #endif
@@ -1401,11 +1404,33 @@ __global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(cons
   const int sh = (int)((uintptr_t)vb & 3u);
   uint4 H0 = make_uint4(0, 0, 0, 0), w = make_uint4(0, 0, 0, 0);
   if (P > 1 && !WGCS_GSO_QLDS && wv != 0) H0 = bld16<false>(hrs, 16 * r);  // the header chunks (Q) of every row
-  if (wv == 0) {
+  // P > 1, a read long enough (WGCS_GSO_SHEAD): the head's inputs through the
+  // scalar path (s_load from uniform addresses), so they do not queue in the
+  // CU's vector-memory pipeline behind the LDS-DMA of the blocks already on
+  // it; the 64 header dwords become per-lane chunks by selects
+  const bool shead = P > 1 && WGCS_GSO_SHEAD && jlen >= 288;  // block-uniform
+  if (wv == 0 && !shead) {
     H0 = bld16<false>(hrs, 16 * r);
     const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(vb - sh), (short)0, (int)(jlen + 3u + (uint32_t)sh), 0x00020000);
     w = bld16<false>(vrs, 0);
+  }
+  if (wv == 0 && shead) {
+    typedef const __attribute__((address_space(4))) uint32_t* cptr;  // constant space: s_load
+    const cptr vp = (cptr)(const void*)(vb - sh);
+    w = make_uint4(vp[0], vp[1], vp[2], vp[3]);
+    const cptr hp = (cptr)(const void*)hbase;
+    uint32_t hv[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) hv[k] = hp[k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {  // lane r of each row takes dwords 4r .. 4r + 3
+      const bool m = r == k;
+      H0.x = m ? hv[4 * k] : H0.x;
+      H0.y = m ? hv[4 * k + 1] : H0.y;
+      H0.z = m ? hv[4 * k + 2] : H0.z;
+      H0.w = m ? hv[4 * k + 3] : H0.w;
+    }
   }
   __builtin_amdgcn_sched_barrier(0);  // keep the header loads ahead of the bulk loads
   // ---- every wave: its share of the whole job into the LDS image.  Chunk q
@@ -1596,9 +1621,15 @@ __global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(cons
         ro.rs = ors;
         ro.dro = (int)(dbase - obase16);
         ro.wt = wt;
+#ifndef WGCS_GSO_PROBE_NOSTREAM  // timing-only builds (not exact output): the row's parts alone
         stream_row_img<U>(img, ib_p, rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, ro);
+#endif
+#ifndef WGCS_GSO_PROBE_NOFINISH
         finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
                    tflags, id0, seq0, &sizes[slot0 + (uint32_t)i], &ro);
+#else
+        if (r == 0) sizes[slot0 + (uint32_t)i] = (int32_t)acc;
+#endif
       } else {
         stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen));
         finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
