@@ -1292,11 +1292,16 @@ struct LdsHead {
   uint4 q[16];  // readBuf[16r, 16r + 16) per row lane r (P > 1 with WGCS_GSO_QLDS)
 };
 
+// Launch shape: P = 3 workgroups of 4 waves per read (round 5, late):
+// 6.35-6.46 us per cfg4 launch on four streams against 6.73-7.31 for one
+// workgroup of 8 waves, 9.72-9.88 against 9.13-9.18 on one stream, the same
+// HBM bytes (profiles/r5_gso_p3_ab*.jsonl, r5_pmc/); several reads in flight
+// (the bench's four streams, a stager's batches) is the regime this serves.
 #ifndef WGCS_GSO_LDS_WAVES
-#define WGCS_GSO_LDS_WAVES 8
+#define WGCS_GSO_LDS_WAVES 4
 #endif
 #ifndef WGCS_GSO_PARTS
-#define WGCS_GSO_PARTS 1  // r5: P = 3 x 4 waves is 4-9 % faster on four streams, 11 % slower on one (r5_gso_parts*)
+#define WGCS_GSO_PARTS 3
 #endif
 #ifndef WGCS_GSO_QLDS
 #define WGCS_GSO_QLDS 1  // P > 1: wave 0 publishes the header chunks through LDS (0: every wave loads them)

@@ -107,9 +107,9 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
         grid = (f"({n_jobs}, {min((max_segs + 15) // 16, 3)}) blocks of 256: one block per (job, group lane), "
                 "looping over segment groups")
     else:
-        kname = "gso_lds_kernel<8,6,true>"
-        grid = (f"{n_jobs} blocks of 512: one workgroup per read, the read staged whole in LDS by LDS-DMA, "
-                "16-lane rows stream its segments out")
+        kname = "gso_lds_kernel<4,6,true,3>"
+        grid = (f"{(n_jobs + 7) // 8 * 8 * 3} blocks of 256: three workgroups per read (dealt to one XCD), each "
+                "staging about a third of the read in LDS by LDS-DMA, 16-lane rows stream its segments out")
     # calibration: a plain device-to-device copy of the super-packet bytes
     # (same read + write volume, same rotation) with the runtime's copy kernel
     with torch.cuda.stream(stream):
