@@ -58,6 +58,9 @@ __device__ __forceinline__ uint4 ld16_nt(const uint8_t* p) {
 #ifndef WGCS_UDP_COAL_ROWS
 #define WGCS_UDP_COAL_ROWS 16  // buffers (16-lane rows) per coalesce block (16: 85 us, 32: 93 us, 64: 102 us on the bench)
 #endif
+#ifndef WGCS_UDP_SPLIT_NT
+#define WGCS_UDP_SPLIT_NT 1  // splitMessages' source windows non-temporal (0: regular loads; A/B builds)
+#endif
 #ifndef WGCS_UDP_NTS
 #define WGCS_UDP_NTS 0
 #endif
@@ -86,7 +89,7 @@ __device__ __forceinline__ void row_copy_dst_aligned(const uint8_t* src, int len
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint8_t* ca = abase + 16 * (k0 + r + 16 * u);
-      A[u] = ca < src_hi ? ld_window<true>(ca, src_hi) : z;
+      A[u] = ca < src_hi ? ld_window<WGCS_UDP_SPLIT_NT != 0>(ca, src_hi) : z;
     }
     uint32_t E = 0;
     if (r == 15) {
