@@ -285,3 +285,22 @@ extern "C" int probe_items_launch(const void* src, size_t bytes, const void* des
   else PI(24, 16);
   return (int)hipGetLastError();
 }
+
+// Shader clock over ~3 us: s_memtime (core clock) against s_memrealtime
+// (100 MHz), one lane; out[0] = clock ticks, out[1] = 100-MHz ticks.
+__global__ void probe_clock(unsigned long long* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long r1;
+  do {
+    r1 = __builtin_amdgcn_s_memrealtime();
+  } while (r1 - r0 < 300);
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  out[0] = t1 - t0;
+  out[1] = r1 - r0;
+}
+extern "C" int probe_clock_launch(void* out, void* stream) {
+  hipLaunchKernelGGL(probe_clock, dim3(1), dim3(64), 0, (hipStream_t)stream, (unsigned long long*)out);
+  return (int)hipGetLastError();
+}
