@@ -61,9 +61,10 @@ torch.cuda.synchronize()
 clk = torch.zeros(2 * (N // W + 1), dtype=torch.int64, device="cuda")
 
 
-def window(k0, launch, slot):
+def window(k0, launch, slot, sync=True):
     """W launches (launch(k, m) enqueues launches k .. k+m-1 on stream 0) with
-    the clock probe after the first half; GPU us per launch, probe excluded."""
+    the clock probe after the first half; GPU us per launch, probe excluded
+    (sync=False: returns the events, read after the whole run)."""
     a, b, c, d = (torch.cuda.Event(enable_timing=True) for _ in range(4))
     a.record(strm[0])
     launch(k0, W // 2)
@@ -72,6 +73,8 @@ def window(k0, launch, slot):
     c.record(strm[0])
     launch(k0 + W // 2, W - W // 2)
     d.record(strm[0])
+    if not sync:
+        return a, b, c, d
     torch.cuda.synchronize()
     return (a.elapsed_time(b) + c.elapsed_time(d)) * 1e3 / W
 
@@ -130,14 +133,28 @@ if AB:
         window(0, f, 0)
     time.sleep(0.1)
     res = {name: ([], []) for name in devs}
-    for rnd in range(int(os.environ.get("SUSTAIN_ROUNDS", "20"))):
+    rounds = int(os.environ.get("SUSTAIN_ROUNDS", "20"))
+    if os.environ.get("SUSTAIN_ASYNC"):  # every window enqueued back to back: no idle between them
+        clk2 = torch.zeros(2 * rounds * len(devs), dtype=torch.int64, device="cuda")
+        clk_saved, clk = clk, clk2
+        evs = []
+        for rnd in range(rounds):
+            for i, (name, f) in enumerate(devs.items()):
+                evs.append((name, window(rnd * W, f, rnd * len(devs) + i, sync=False)))
+        torch.cuda.synchronize()
+        c = clk.cpu().numpy()
+        for j, (name, (a, b, cc, d)) in enumerate(evs):
+            res[name][0].append(round((a.elapsed_time(b) + cc.elapsed_time(d)) * 1e3 / W, 2))
+            res[name][1].append(round(100.0 * c[2 * j] / max(c[2 * j + 1], 1)))
+        rounds = 0
+    for rnd in range(rounds):
         for i, (name, f) in enumerate(devs.items()):
             clk.zero_()
             res[name][0].append(round(window(rnd * W, f, 0), 2))
             c = clk.cpu().numpy()
             res[name][1].append(round(100.0 * c[0] / max(c[1], 1)))
     for name, (us, mhz) in res.items():
-        print(json.dumps({"variant": name, "spec": dict(x.split("=", 1) for x in AB.split(";"))[name],
+        print(json.dumps({"variant": name, "async": bool(os.environ.get("SUSTAIN_ASYNC")), "spec": dict(x.split("=", 1) for x in AB.split(";"))[name],
                           "us_per_launch": us, "sclk_mhz": mhz}), flush=True)
     sys.exit(0)
 LAUNCH = {"flat": flat, "cs1": cs_launcher(dev), "cs1_bpc16": cs_launcher(dev16), "rowsg": rowsg}
