@@ -144,6 +144,35 @@ def test_recorded_eight_rank_rehearsal():
     assert line["cpu_baseline"]["value"] > 0
 
 
+def test_recorded_final_driver_lines_agree_with_rocprof():
+    """The round-5 close-out (scripts/r5_final3.sh): the driver's command,
+    recorded twice on the final tree, gives complete lines, and their
+    one-stream kernel time agrees with the committed rocprofv3 one-stream
+    average at the same step count (profiles/r5_final3_cfg2_1s_20*_kernel_stats.csv)
+    within 5 %."""
+    import csv
+
+    fn = os.path.join(ROOT, "profiles", "r5_final3_lines.jsonl")
+    if not os.path.exists(fn):
+        pytest.skip("final lines not recorded yet")
+    lines = [json.loads(l) for l in open(fn) if l.startswith("{")]
+    drv = [l for l in lines if l["tag"].startswith("cfg2_driver")]
+    assert len(drv) == 2
+    prof_us = []
+    for tag in ("20a", "20b"):
+        with open(os.path.join(ROOT, "profiles", f"r5_final3_cfg2_1s_{tag}_kernel_stats.csv")) as f:
+            rows = [r for r in csv.DictReader(f) if "checksum_batch_kernel" in r["Name"]]
+        assert len(rows) == 1 and int(rows[0]["Calls"]) == 45  # 20 + 5 launches, one stream
+        prof_us.append(float(rows[0]["AverageNs"]) / 1e3)
+    for line in drv:
+        line = {k: v for k, v in line.items() if k != "tag"}
+        assert bench.line_problems(line) == []
+        r = line["roofline"]
+        assert r["traffic"] is not None and line["cpu_baseline"]["value"] > 0
+        one_us = r["kernel_ms_one_stream"] * 1e3
+        assert all(abs(one_us - p) / p < 0.05 for p in prof_us), (one_us, prof_us)
+
+
 def test_numa_helpers(tmp_path):
     from wireguard_amd import shard
 
