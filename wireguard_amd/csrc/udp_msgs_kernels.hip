@@ -61,6 +61,9 @@ __device__ __forceinline__ uint4 ld16_nt(const uint8_t* p) {
 #ifndef WGCS_UDP_SPLIT_NT
 #define WGCS_UDP_SPLIT_NT 1  // splitMessages' source windows non-temporal (0: regular loads; A/B builds)
 #endif
+#ifndef WGCS_UDP_SPLIT_EDGE_T
+#define WGCS_UDP_SPLIT_EDGE_T 0  // 1: windows in a 128-B line the row shares with its neighbours load temporal
+#endif
 #ifndef WGCS_UDP_NTS
 #define WGCS_UDP_NTS 0
 #endif
@@ -89,7 +92,15 @@ __device__ __forceinline__ void row_copy_dst_aligned(const uint8_t* src, int len
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint8_t* ca = abase + 16 * (k0 + r + 16 * u);
-      A[u] = ca < src_hi ? ld_window<WGCS_UDP_SPLIT_NT != 0>(ca, src_hi) : z;
+      if (WGCS_UDP_SPLIT_EDGE_T) {
+        // the first and last lines of a packet are the neighbouring packets'
+        // too: loaded temporal they stay in L2 for the other row's read
+        const uintptr_t line = (uintptr_t)ca & ~(uintptr_t)127;
+        const bool shared = line < (uintptr_t)src || line + 128 > (uintptr_t)src_hi;
+        A[u] = ca >= src_hi ? z : shared ? ld_window<false>(ca, src_hi) : ld_window<WGCS_UDP_SPLIT_NT != 0>(ca, src_hi);
+      } else {
+        A[u] = ca < src_hi ? ld_window<WGCS_UDP_SPLIT_NT != 0>(ca, src_hi) : z;
+      }
     }
     uint32_t E = 0;
     if (r == 15) {
