@@ -106,8 +106,11 @@ __device__ __forceinline__ uint4 wave_desc(const uint4* __restrict__ pkts, uint3
   return r;
 }
 
+#ifndef WGCS_CS_BLOCK
+#define WGCS_CS_BLOCK 256  // threads per block (A/B builds: 512, 1024)
+#endif
 template <int MODE, int G, int U, bool NT>
-__global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict__ arena,
+__global__ __launch_bounds__(WGCS_CS_BLOCK) void checksum_batch_kernel(uint8_t* __restrict__ arena,
                                                              const uint4* __restrict__ pkts,
                                                              const uint64_t* __restrict__ initial,
                                                              uint32_t n, void* __restrict__ out,
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(256) void checksum_batch_kernel(uint8_t* __restrict
 template <int MODE>
 static hipError_t launch_mode(uint8_t* arena, const wgcs_pkt* pkts, const uint64_t* init, uint32_t n, void* out,
                               int inplace, hipStream_t s, int num_cu, const LaunchTuning& t) {
-  const int ppb = (64 / t.lanes_per_pkt) * 4;  // packets per block per step
+  const int ppb = (64 / t.lanes_per_pkt) * (WGCS_CS_BLOCK / 64);  // packets per block per step
   long want = ((long)n + ppb - 1) / ppb;
   want = (want + 7) & ~7L;  // a multiple of 8 keeps the XCD-aware order (blocks past n exit at once)
   long cap = (long)num_cu * t.blocks_per_cu;
@@ -269,10 +272,10 @@ static hipError_t launch_mode(uint8_t* arena, const wgcs_pkt* pkts, const uint64
 #define WGCS_LAUNCH(G, U)                                                                                    \
   do {                                                                                                      \
     if (t.nt)                                                                                               \
-      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, true>), dim3(grid), dim3(256), 0, s, arena, d,  \
+      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, true>), dim3(grid), dim3(WGCS_CS_BLOCK), 0, s, arena, d, \
                          init, n, out, inplace, amask, xcd);                                                \
     else                                                                                                    \
-      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, false>), dim3(grid), dim3(256), 0, s, arena, d, \
+      hipLaunchKernelGGL((checksum_batch_kernel<MODE, G, U, false>), dim3(grid), dim3(WGCS_CS_BLOCK), 0, s, arena, d, \
                          init, n, out, inplace, amask, xcd);                                                \
   } while (0)
   if (t.lanes_per_pkt == 64) {
