@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/${TAG:-r5_cs_block}; mkdir -p $OUT
-LIBS="wireguard_amd/libwgcsum.so scripts/probe_so/libwgcsum_csblk512.so scripts/probe_so/libwgcsum_csblk1024.so"
+LIBS=${LIBS:-"wireguard_amd/libwgcsum.so scripts/probe_so/libwgcsum_csblk512.so scripts/probe_so/libwgcsum_csblk1024.so"}
 T="tests/test_gpu_checksum.py tests/test_gpu_batches.py tests/test_gpu_fullsize.py"
 for lib in $LIBS; do
   name=$(basename $lib .so)
