@@ -91,9 +91,10 @@ def parse():
                     help="poll the closing event before torch.cuda.synchronize() (slower: profiles/r4_probe_poll_ab.jsonl)")
     ap.add_argument("--no-affinity", action="store_true", help="do not bind each rank to its GPU's NUMA-local CPUs")
     ap.add_argument("--warm-ms", type=float, default=40.0,
-                    help="configs[4] legs (cfg5_strong, --config cfg5): keep issuing warmup steps for at least this "
-                         "much wall time after the W contract steps (the chip streams ~15 %% slower for ~25 ms after "
-                         "idling; profiles/r5_cfg5_regions.jsonl); 0 = W steps only")
+                    help="configs[4] legs (cfg5_strong, --config cfg5): AFTER the contract region (K steps behind "
+                         "exactly W warmup steps, which is `value`), keep issuing untimed steps for at least this "
+                         "much wall time and time the K steps again as the diagnostic `value_warm` (the chip streams "
+                         "~15 %% slower for ~25 ms after idling; profiles/r5_cfg5_regions.jsonl); 0 = no warm re-time")
     ap.add_argument("--repeat", type=int, default=1,
                     help="diagnostics: time the K-step region this many times; `value` stays the FIRST region, "
                          "the others are listed under timing.repeats")
@@ -289,9 +290,12 @@ def main():
                 "wall_us": round(uw * 1e6, 2), "GiB_per_s": round(bytes_per_step * args.steps / uw / 2**30, 2)}
             if um is not None:
                 result["timing"]["ungated"]["event_span_us"] = round(um * args.steps * 1e3, 2)
-        if leg.get("prewarm"):
-            result["timing"]["prewarm"] = {"warm_ms": args.warm_ms, "launches": leg["prewarm"],
-                                           "what": "untimed warmup launches beyond the W contract steps (--warm-ms)"}
+        if leg.get("warm"):
+            ww, wm = leg["warm"]
+            wel = shard.max_over_ranks(ww, dist, device=red_dev)
+            result["value_cold"] = result["value"]
+            result["value_warm"] = round(total_bytes / wel / 2**30, 2)
+            result["timing"]["warm"] = warm_block(args.warm_ms, leg["prewarm"], ww, wm, args.steps)
         if leg["repeats"]:
             result["timing"]["repeats"] = [{"wall_us": round(w * 1e6, 1), "event_span_us": round(m * args.steps * 1e3, 1)}
                                            for w, m in leg["repeats"]]
@@ -324,12 +328,15 @@ REQUIRED_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per
                  "scaling", "vs_baseline", "dtype", "data", "config")
 
 
-def line_problems(line: dict) -> list[str]:
+def line_problems(line: dict, require_cold: bool = True) -> list[str]:
     """What is missing from a cfg2 result line (the driver's default
     invocation), per the bench contract: the required keys, `roofline`,
     `cpu_baseline` at every N, and for N > 1 every rank's kernel time, the
     process group's world size and the `cfg5_strong` block (BASELINE.json
-    configs[4]) with its own roofline.  Empty = complete."""
+    configs[4]) with its own roofline and (round 6) its
+    cold value -- the K steps behind exactly W warmup steps -- as `value` and
+    `value_cold`, any warm re-time only beside them.  Empty = complete.
+    require_cold=False reads lines recorded before round 6."""
     bad = [f"missing {k}" for k in REQUIRED_KEYS if k not in line]
     if bad:
         return bad
@@ -358,6 +365,11 @@ def line_problems(line: dict) -> list[str]:
             bad.append("cfg5_strong: n_gpus / scaling / value")
         if len(st.get("packets_per_rank", [])) != n or sum(st.get("packets_per_rank", [])) != CONFIGS["cfg5"][0]:
             bad.append("cfg5_strong.packets_per_rank must cover the 1M batch")
+        if require_cold:
+            if st.get("value_cold") != st.get("value"):
+                bad.append("cfg5_strong.value_cold must be the contract value (K steps behind exactly W warmups)")
+            if "value_warm" in st and "warm" not in st:
+                bad.append("cfg5_strong.value_warm without its warm block")
         srf = st.get("roofline")
         if not srf or "frac" not in srf or (n > 1 and len(srf.get("kernel_ms_per_rank", [])) != n):
             bad.append("cfg5_strong.roofline missing or without every rank")
@@ -401,6 +413,19 @@ def roofline(kname, bytes_per_step, flen, n, kern_ms, S, iso_ms, kern_all=None) 
         r["kernel_ms_one_stream"] = round(iso_ms, 5)
         r["frac_one_stream"] = round(bytes_per_step / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     return r
+
+
+def gate_streams(dev, bell, streams, use_events) -> list:
+    """Post the doorbell wait (wgcs_stream_wait_flag on bell[0] == 1) on the
+    launch streams of a gated region and return the streams that wait on it.
+    With the bracket events on, streams[1:] wait on e0, which is recorded on
+    stream 0 behind the bell, so stream 0 alone is gated; without events
+    nothing else would hold them before the clock starts, so each waits on the
+    bell itself (tests/test_gpu_abi_safety.py drives this helper)."""
+    gated = list(streams[:1]) if use_events else list(streams)
+    for s in gated:
+        dev.stream_wait_flag(s, bell, 1)
+    return gated
 
 
 def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, rotate, barrier, use_events,
@@ -456,12 +481,7 @@ def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, ro
         evs = (e0 if use_events else None, e1 if use_events else None)
         if bell is not None and gated:
             bell[0] = 0
-            # with the bracket events on, streams[1:] wait on e0, recorded on
-            # stream 0 behind the bell; without events nothing else would hold
-            # them before the clock starts, so each waits on the bell itself
-            # 
-            for s in (strm[:1] if use_events else strm[:ns]):
-                dev.stream_wait_flag(s, bell, 1)
+            gate_streams(dev, bell, strm[:ns], use_events)
             try:
                 dev.checksum_batches(mode, bl, strm[:ns], *evs)
             finally:
@@ -498,21 +518,6 @@ def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, ro
         dev.checksum_batches(mode, batches(warmup, 0), strm, e0 if use_events else None,
                              e1 if use_events else None)
     torch.cuda.synchronize()
-    # Large launches (configs[4]: 1.57 GB each at N = 1) run ~15 % slower for
-    # the first ~25 ms of sustained streaming after the GPU sat idle (the
-    # process builds the 1 M-frame batch on the CPU first): the same 20-step
-    # region timed 4 times in a row reads 267 / 258 / 238 / 227 us per launch
-    # (profiles/r5_cfg5_regions.jsonl).  Such legs keep issuing warmup steps,
-    # in the same enqueue shape, for at least warm_ms of wall time beyond the
-    # W contract steps; the timed region is still exactly K steps.
-    prewarm = 0
-    if warm_ms > 0:
-        t_end = time.perf_counter() + warm_ms / 1e3
-        while time.perf_counter() < t_end:
-            dev.checksum_batches(mode, batches(8, warmup + prewarm), strm)
-            torch.cuda.synchronize()
-            prewarm += 8
-        warmup += prewarm
     if verify:
         if mode == MODE_VALIDATE:
             assert bool(outs[0][:n].all().item()), "VALIDATE: synthetic frames must all be valid"
@@ -525,6 +530,23 @@ def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, ro
 
     local_elapsed, kern_ms = timed(steps, warmup, S)
     repeats = [timed(steps, warmup + r * steps, S) for r in range(1, repeat)]
+    # Large launches (configs[4]: 1.57 GB each at N = 1) run ~15 % slower for
+    # the first ~25 ms of sustained streaming after the GPU sat idle (the
+    # process builds the 1 M-frame batch on the CPU first): the same 20-step
+    # region timed 4 times in a row reads 267 / 258 / 238 / 227 us per launch
+    # (profiles/r5_cfg5_regions.jsonl).  The contract region above ran after
+    # exactly W warmup steps (`value`, cold); such legs then keep issuing
+    # untimed steps, in the same enqueue shape, for at least warm_ms of wall
+    # time and time the same K steps again (`value_warm`, a diagnostic).
+    prewarm, warm = 0, None
+    if warm_ms > 0:
+        k0 = warmup + repeat * steps
+        t_end = time.perf_counter() + warm_ms / 1e3
+        while time.perf_counter() < t_end:
+            dev.checksum_batches(mode, batches(8, k0 + prewarm), strm)
+            torch.cuda.synchronize()
+            prewarm += 8
+        warm = timed(steps, k0 + prewarm, S)
     # The same K steps enqueued inside the clock (no doorbell), after the
     # timed region: the rounds before round 4 timed this way, so the line
     # carries both wall times for comparison (never `value`)
@@ -535,7 +557,7 @@ def checksum_leg(torch, dev, arena_np, pkts_np, mode, steps, warmup, streams, ro
         _, iso_ms = timed(max(steps, 20), warmup + steps, 1)
     del arenas, outs, pkts
     return {"elapsed": local_elapsed, "kern_ms": kern_ms, "iso_ms": iso_ms, "repeats": repeats, "streams": S, "R": R,
-            "ungated": ungated, "prewarm": prewarm}
+            "ungated": ungated, "prewarm": prewarm, "warm": warm}
 
 
 def strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_events) -> dict:
@@ -545,7 +567,9 @@ def strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_
     two streams like the headline's (at N = 8 a rank's launch is ~35 us, and
     consecutive launches then overlap their ramp and drain; at N = 1 the
     0.27-ms launches neither gain nor lose).  Value = the whole batch's
-    bytes x K / the slowest rank's wall time."""
+    bytes x K / the slowest rank's wall time, over the K steps behind exactly
+    W warmup steps (`value_cold`, the same number); `value_warm` re-times them
+    after --warm-ms of untimed steps."""
     from wireguard_amd import shard
 
     n_cfg, flen, kinds, cfg_idx, _ = CONFIGS["cfg5"]
@@ -570,13 +594,32 @@ def strong_leg(torch, dev, args, mode, rank, world, barrier, dist, red_dev, use_
         "packets_per_rank": [int(x) for x in ranges],
         "streams": leg["streams"],
         "rotated_copies": leg["R"],
-        "prewarm": {"warm_ms": args.warm_ms, "launches": leg["prewarm"],
-                    "what": "untimed warmup launches beyond the W contract steps (--warm-ms)"},
     }
+    out["value_cold"] = out["value"]
     if leg["kern_ms"] is not None:
         out["roofline"] = roofline(kernel_name(mode), bytes_rank, flen, hi - lo, leg["kern_ms"], leg["streams"], None,
                                    kern_all)
+    if leg.get("warm"):  # the diagnostic re-time after --warm-ms of untimed steps (every rank takes part)
+        ww, wm = leg["warm"]
+        wel = shard.max_over_ranks(ww, dist, device=red_dev)
+        wk_all = shard.gather_floats(wm if wm is not None else -1.0, dist, device=red_dev)
+        out["value_warm"] = round(n_cfg * flen * args.steps / wel / 2**30, 2)
+        out["warm"] = warm_block(args.warm_ms, leg["prewarm"], ww, wm, args.steps)
+        if wm is not None:
+            out["warm"]["roofline"] = roofline(kernel_name(mode), bytes_rank, flen, hi - lo, wm, leg["streams"], None,
+                                               wk_all)
     return out
+
+
+def warm_block(warm_ms, launches, wall, kern_ms, steps) -> dict:
+    """timing of the K steps re-run after `launches` untimed prewarm steps
+    (--warm-ms): a diagnostic beside the contract's cold `value`."""
+    b = {"warm_ms": warm_ms, "prewarm_launches": launches, "wall_us": round(wall * 1e6, 2),
+         "what": "the same K steps timed again after the contract region and --warm-ms of untimed steps "
+                 "(a warm chip); `value` is the region after exactly W warmup steps"}
+    if kern_ms is not None:
+        b["event_span_us"] = round(kern_ms * steps * 1e3, 2)
+    return b
 
 
 def _tune_tag():

@@ -76,7 +76,9 @@ def _line(n, with_strong=True, with_cpu=True):
         line["cpu_baseline"] = {"value": 8.8, "unit": "GiB/s", "cores": 1, "kind": "port", "sample": "s"}
     if with_strong:
         per = [1048576 * (r + 1) // n - 1048576 * r // n for r in range(n)]
-        line["cfg5_strong"] = {"value": 5000.0 * n, "n_gpus": n, "scaling": "strong", "packets_per_rank": per,
+        line["cfg5_strong"] = {"value": 5000.0 * n, "value_cold": 5000.0 * n, "value_warm": 5400.0 * n,
+                               "warm": bench.warm_block(40.0, 176, 0.0045, 0.21, 20),
+                               "n_gpus": n, "scaling": "strong", "packets_per_rank": per,
                                "roofline": bench.roofline("k", per[0] * 1500, 1500, per[0], 0.27 / n, 1, None,
                                                           [0.27 / n] * n)}
     return line
@@ -97,6 +99,16 @@ def test_line_schema_complete(n):
 @pytest.mark.parametrize("n", [1, 4])
 def test_line_schema_flags_gaps(n):
     assert "missing cfg5_strong" in bench.line_problems(_line(n, with_strong=False))
+    # the configs[4] block's `value` is the cold region (K
+    # steps behind exactly W warmups), carried again as value_cold; a warm
+    # re-time only beside it
+    line = _line(n)
+    line["cfg5_strong"]["value"] = line["cfg5_strong"]["value_warm"]
+    assert any("value_cold" in p for p in bench.line_problems(line))
+    line = _line(n)
+    del line["cfg5_strong"]["value_cold"]
+    assert any("value_cold" in p for p in bench.line_problems(line))
+    assert bench.line_problems(line, require_cold=False) == []
     assert "cpu_baseline missing or incomplete" in bench.line_problems(_line(n, with_cpu=False))
     if n > 1:
         line = _line(n)
@@ -116,12 +128,13 @@ def test_recorded_rehearsal_lines_complete():
     if not files:
         pytest.skip("no rehearsal lines recorded yet")
     for fn in files:
+        pre6 = os.path.basename(fn)[:2] in ("r4", "r5")  # recorded before value_cold existed
         with open(fn) as f:
             for l in f:
                 if l.startswith("{"):
                     line = json.loads(l)
                     assert line["n_gpus"] > 1
-                    assert bench.line_problems(line) == [], fn
+                    assert bench.line_problems(line, require_cold=not pre6) == [], fn
 
 
 def test_recorded_eight_rank_rehearsal():
@@ -137,7 +150,7 @@ def test_recorded_eight_rank_rehearsal():
     lines = [json.loads(l) for l in open(fn) if l.startswith("{")]
     assert len(lines) == 1
     line = lines[0]
-    assert bench.line_problems(line) == []
+    assert bench.line_problems(line, require_cold=False) == []
     assert line["n_gpus"] == 8 and line["config"]["dist"]["world_size"] == 8
     assert len(line["roofline"]["kernel_ms_per_rank"]) == 8
     assert len(line["cfg5_strong"]["packets_per_rank"]) == 8
@@ -166,7 +179,7 @@ def test_recorded_final_driver_lines_agree_with_rocprof():
         prof_us.append(float(rows[0]["AverageNs"]) / 1e3)
     for line in drv:
         line = {k: v for k, v in line.items() if k != "tag"}
-        assert bench.line_problems(line) == []
+        assert bench.line_problems(line, require_cold=False) == []
         r = line["roofline"]
         assert r["traffic"] is not None and line["cpu_baseline"]["value"] > 0
         one_us = r["kernel_ms_one_stream"] * 1e3
@@ -248,3 +261,20 @@ def test_bench_default_line_complete():
     assert line["roofline"]["kernel_ms"] <= line["ms_per_step"] * 1.05
     st = line["cfg5_strong"]
     assert st["packets_per_rank"] == [1048576] and st["roofline"]["frac"] > 0
+
+
+def test_gate_streams_helper():
+    """bench.gate_streams (the timed region's doorbell set-up): with bracket
+    events only stream 0 waits on the bell (the others wait on e0 behind it);
+    without events every launch stream waits on it itself."""
+    class Dev:
+        def __init__(self):
+            self.calls = []
+
+        def stream_wait_flag(self, s, bell, value):
+            self.calls.append((s, value))
+
+    for use_events, want in ((True, ["s0"]), (False, ["s0", "s1", "s2"])):
+        d = Dev()
+        got = bench.gate_streams(d, object(), ["s0", "s1", "s2"], use_events)
+        assert got == want and [c[0] for c in d.calls] == want and all(c[1] == 1 for c in d.calls)

@@ -213,10 +213,16 @@ def test_doorbell_gates_every_stream_without_events(dev):
     """bench.py's gate with --no-event-timing and two launch streams: every
     launch stream waits on the doorbell itself, so no batch of the series runs
     before the ring even with no bracket events joining the streams (ADVICE
-    r4: only stream 0 used to be gated)."""
+    r4: only stream 0 used to be gated).  The gate is bench.gate_streams, the
+    helper bench.py's timed region calls."""
+    import os
+    import sys
     import time
 
     import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
 
     import oracle
     from wireguard_amd import synth
@@ -230,8 +236,8 @@ def test_doorbell_gates_every_stream_without_events(dev):
     bell = dev.host_alloc(64).view(np.uint32)
     torch.cuda.synchronize()
     bell[0] = 0
-    for s in streams:
-        dev.stream_wait_flag(s, bell, 1)
+    gated = bench.gate_streams(dev, bell, streams, use_events=False)
+    assert len(gated) == len(streams)
     dev.checksum_batches(MODE_VALIDATE, dev.batch_list([(d_arena, d_pkts, 512, o) for o in outs]), streams)
     evs = [torch.cuda.Event() for _ in streams]
     for e, s in zip(evs, streams):

@@ -1683,8 +1683,10 @@ hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs
       hipLaunchKernelGGL((gso_lds_kernel<NW, WGCS_GSO_U, true, 1>), dim3(n_jobs), dim3(NW * 64), 0, s, arena, jobs,
                          max_segs, out, out_stride, outpos, offset, room, sizes, count, status, n_jobs);
     } else {  // (n_jobs rounded up to 8) x P blocks
-      if ((uint64_t)(n_jobs + 7u) / 8u * 8u * P > 0x7FFFFFFFull) return hipErrorInvalidValue;
-      hipLaunchKernelGGL((gso_lds_kernel<NW, WGCS_GSO_U, true, P>), dim3((n_jobs + 7u) / 8u * 8u * P), dim3(NW * 64), 0,
+      // in 64 bits before the check (n_jobs + 7 wrapped in 32)
+      const uint64_t nblk = ((uint64_t)n_jobs + 7u) / 8u * 8u * (uint64_t)P;
+      if (nblk > 0x7FFFFFFFull) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((gso_lds_kernel<NW, WGCS_GSO_U, true, P>), dim3((uint32_t)nblk), dim3(NW * 64), 0,
                          s, arena, jobs, max_segs, out, out_stride, outpos, offset, room, sizes, count, status, n_jobs);
     }
     return hipGetLastError();
