@@ -1254,6 +1254,87 @@ __device__ __forceinline__ uint32_t img4(const uint8_t* img, int o) {
   return *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(img + o, 4));
 }
 
+// ---- the staged image (round 6).  One loader wave issues every LDS-DMA load
+// of a part itself, through inline asm: hipcc's wait-count pass then does not
+// know that LDS-DMA is pending, so it puts no vmcnt(0) in front of the LDS
+// accesses that follow (with the builtin it waits for the whole image before
+// the first one).  The loader publishes its progress stage by stage -- a
+// counted `s_waitcnt vmcnt(N)` (its own DMA only: it issues no vector store
+// before its last wait) and then an LDS word -- and the row waves poll that
+// word, so the rows of the first segments stream out while the later bytes
+// of the read are still landing.
+typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+// Buffer resource words (wave-uniform): base, stride 0, num_records, the
+// same config dword as __builtin_amdgcn_make_buffer_rsrc(..., 0x00020000).
+__device__ __forceinline__ u32x4s rsrc_words(const void* base, uint32_t nrec) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  return u32x4s{(uint32_t)ufl((int)(uint32_t)a), (uint32_t)ufl((int)((uint32_t)(a >> 32) & 0xFFFFu)),
+                (uint32_t)ufl((int)nrec), 0x00020000u};
+}
+// The LDS byte address of a __shared__ object (what M0 takes).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)ufl((int)(uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p);
+}
+// buffer_load_dwordx4 ... lds: 16 bytes per lane from rsrc + voff into LDS at
+// m0v + 16 * lane (the builtin's instruction, issued where hipcc cannot see it).
+template <bool NT>
+__device__ __forceinline__ void dma16_asm(const u32x4s& rs, int voff, uint32_t m0v) {
+  if (NT)
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen nt lds" ::"v"(voff), "s"(rs), "s"(m0v)
+                 : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(m0v)
+                 : "memory", "m0");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N <= 63, "gfx9 vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// The loader's stage waits: after DMA [0, T) of K have landed (its vmcnt
+// down to K - T), T is stored in the LDS word; every D instructions.
+// The stage word: relaxed workgroup-scope atomics on an LDS pointer (plain
+// ds_read_b32 / ds_write_b32; a volatile or flat access gets a vmcnt(0)
+// from the memory legalizer, which would wait for the whole image).
+typedef __attribute__((address_space(3))) int32_t* lds_flag_t;
+__device__ __forceinline__ void flag_put(lds_flag_t f, int v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int flag_get(lds_flag_t f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <int K, int D, int S>
+__device__ __forceinline__ void publish_stages(lds_flag_t landed, int lane) {
+  if constexpr (S < K) {
+    constexpr int T = S + D < K ? S + D : K;
+    vm_wait<K - T>();
+    if (lane == 0) flag_put(landed, T);
+    publish_stages<K, D, T>(landed, lane);
+  }
+}
+
+// The loader, throttled: at most W of its image DMA instructions in flight
+// (W KiB; three loaders per CU), so that the chip's memory queues stay
+// shallow -- every CU dumping its whole image at once queues ~18 MB, and a
+// request issued behind that (the head's input, a stage's bytes) waits ~3 us
+// for it.  The header DMA (issued before the call) is waited first and
+// published as `hland`; then DMA d is issued once DMA d - W has landed, and
+// `landed` counts landed instructions in steps of D.
+template <int K, int W, int D, int d>
+__device__ __forceinline__ void loader_issue(const u32x4s& rs, uint32_t l0, int lane, lds_flag_t landed) {
+  if constexpr (d < K) {
+    constexpr int done = d - W + 1;  // DMA [0, done) landed after this wait (the header DMA too)
+    if constexpr (done > 0) {
+      vm_wait<W - 1>();
+      if constexpr (done % D == 0) {
+        if (lane == 0) flag_put(landed, done);
+      }
+    }
+    dma16_asm<true>(rs, 16 * (64 * d + lane), l0 + 1024 * d);
+    loader_issue<K, W, D, d + 1>(rs, l0, lane, landed);
+  }
+}
+
 // load_windows from the LDS image (job byte x at image offset ibias + x).
 // Unlike the HBM form, windows outside the row's payload bytes [lo, hi) are
 // read too (from LDS, no memory traffic) and not zeroed: consume_batch masks
@@ -1284,12 +1365,29 @@ __device__ __forceinline__ void stream_row_img(const uint8_t* img, int ibias, co
   }
 }
 
-// The head's results, published by wave 0 through LDS.
+// The head's inputs: the header chunks (lane r of each row: readBuf[16r, 16r +
+// 16) from the dword holding it) and the 16 bytes from the dword holding vb[0].
+struct HeadIn {
+  uint4 H0, w;
+};
+// The head's results in registers (wave-uniform except Q: lane r of each
+// row holds readBuf[16r, 16r + 16)).
+struct HeadRes {
+  int clean, type, ipv, hdr_len, gso, cs, co, plen;
+  uint32_t ip_base, l4_base, tflags, id0, seq0;
+  uint4 Q;
+};
+// The head's results, published by the head wave through LDS.
 struct LdsHead {
   int32_t clean;  // 1: the row-streaming path (a clean job, gso_rows_kernel's criterion)
   int32_t type, ipv, hdr_len, gso, cs, co, plen;
   uint32_t ip_base, l4_base, tflags, id0, seq0;
   uint4 q[16];  // readBuf[16r, 16r + 16) per row lane r (P > 1 with WGCS_GSO_QLDS)
+  int32_t landed;           // staged: the loader's DMA instructions landed so far
+  int32_t hready;           // staged: 1 once the head wave has published everything above
+  int32_t hland;            // staged: 1 once the loader's header DMA (hbuf) has landed
+  int32_t hgeo;             // staged: 1 once the head wave has published the verdict and geometry
+  uint4 hbuf[64];           // staged: the read's first KiB from its 16-B aligned start (the head's input)
 };
 
 // Launch shape: P = 3 workgroups of 4 waves per read (round 5, late):
@@ -1308,6 +1406,15 @@ struct LdsHead {
 #endif
 #ifndef WGCS_GSO_SHEAD
 #define WGCS_GSO_SHEAD 1  // P > 1: the head's loads through the scalar path
+#endif
+#ifndef WGCS_GSO_STAGED
+#define WGCS_GSO_STAGED 0  // P > 1: 1 = one loader wave, the image published stage by stage (round 6 A/B; slower)
+#endif
+#ifndef WGCS_GSO_STAGE_DMA
+#define WGCS_GSO_STAGE_DMA 2  // staged: LDS-DMA instructions (KiB) per published stage
+#endif
+#ifndef WGCS_GSO_INFLIGHT
+#define WGCS_GSO_INFLIGHT 8  // staged: the loader's image DMA instructions (KiB) in flight at once
 #endif
 #ifndef WGCS_GSO_PART_XCD
 #define WGCS_GSO_PART_XCD 1  // P > 1: a job's parts on one XCD (0: consecutive blocks)
@@ -1398,7 +1505,15 @@ __global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(cons
   const bool use_img = P == 1 ? (jlen >= 14 && nch <= kImgBytes / 16)  // block-uniform
                               : (jlen >= 14 && q_n <= kStage / 16);
   const bool raw = (job.flags & WGCS_GSO_JOB_RAW) != 0;
-  // ---- wave 0: header chunks (as gso_rows_kernel) and the virtio header +
+  // Staged (P > 1, round 6): wave 0 is the loader and issues nothing else
+  // before its stage waits; wave 1 runs the head (its loads are the
+  // compiler's, waited on inside the head: none is pending where the loader's
+  // code continues, so hipcc puts no vmcnt(0) behind the loader's DMA).
+  constexpr bool STG = P > 1 && WGCS_GSO_STAGED != 0;
+  constexpr int kHeadWave = STG ? 1 : 0;
+  constexpr int kDma = (kStage + 1023) / 1024;  // staged: the loader's LDS-DMA instructions (1 KiB each)
+  static_assert(!STG || (NW >= 2 && kDma <= 63 && kDma * 1024 <= kArr), "staged image: roles, vmcnt, image size");
+  // ---- the head wave (wave 0; staged: wave 1): header chunks (as gso_rows_kernel) and the virtio header +
   // readBuf[0] (16 bytes from the dword holding vb[0], range-checked: zeros
   // past the job), issued ahead of its bulk loads so that the head waits for
   // them alone (a counted vmcnt)
@@ -1408,19 +1523,34 @@ __global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(cons
       const_cast<uint8_t*>(hbase), (short)0, (int)(jlen + 3u) - (int)(hbase - vb), 0x00020000);
   const int sh = (int)((uintptr_t)vb & 3u);
   uint4 H0 = make_uint4(0, 0, 0, 0), w = make_uint4(0, 0, 0, 0);
-  if (P > 1 && !WGCS_GSO_QLDS && wv != 0) H0 = bld16<false>(hrs, 16 * r);  // the header chunks (Q) of every row
+  if (P > 1 && !WGCS_GSO_QLDS && wv != kHeadWave) H0 = bld16<false>(hrs, 16 * r);  // the header chunks (Q) of every row
   // P > 1, a read long enough (WGCS_GSO_SHEAD): the head's inputs through the
   // scalar path (s_load from uniform addresses), so they do not queue in the
   // CU's vector-memory pipeline behind the LDS-DMA of the blocks already on
   // it; the 64 header dwords become per-lane chunks by selects
   const bool shead = P > 1 && WGCS_GSO_SHEAD && jlen >= 288;  // block-uniform
-  if (wv == 0 && !shead) {
+  // (by value in and out: a lambda writing the outer H0 / w by reference put
+  // them in scratch memory, whose loads then queued behind the bulk DMA)
+  auto head_loads = [&]() -> HeadIn {
+  uint4 H0 = make_uint4(0, 0, 0, 0), w = make_uint4(0, 0, 0, 0);
+  if (STG && shead) {
+    // staged: the loader's first DMA instruction brings the read's first KiB
+    // into hd.hbuf ahead of its bulk; the head reads its inputs from there
+    // (s_load's of the same bytes queue behind every CU's bulk DMA: ~3 us)
+    while (ufl(flag_get((lds_flag_t)&hd.hland)) == 0) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+#if defined(WGCS_GSO_STAMPS) && WGCS_GSO_STAMPS == 3  // head wave: T2 header seen
+    stp[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+    const uint8_t* hb8 = reinterpret_cast<const uint8_t*>(hd.hbuf);
+    w = img16(hb8, ibias - sh);
+    H0 = img16(hb8, ibias + 10 - hph + 16 * r);
+  } else if (!shead) {
     H0 = bld16<false>(hrs, 16 * r);
     const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(vb - sh), (short)0, (int)(jlen + 3u + (uint32_t)sh), 0x00020000);
     w = bld16<false>(vrs, 0);
-  }
-  if (wv == 0 && shead) {
+  } else {
     typedef const __attribute__((address_space(4))) uint32_t* cptr;  // constant space: s_load
     const cptr vp = (cptr)(const void*)(vb - sh);
     w = make_uint4(vp[0], vp[1], vp[2], vp[3]);
@@ -1437,7 +1567,8 @@ __global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(cons
       H0.w = m ? hv[4 * k + 3] : H0.w;
     }
   }
-  __builtin_amdgcn_sched_barrier(0);  // keep the header loads ahead of the bulk loads
+  return HeadIn{H0, w};
+  };
   // ---- every wave: its share of the whole job into the LDS image.  Chunk q
   // = the aligned 16 bytes at (vb & ~15) + 16 q, image offset 16 q (job byte x
   // at ibias + x); an aligned chunk holding a job byte lies in that byte's
@@ -1445,7 +1576,27 @@ __global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(cons
   // range-checked resource over the job's chunks (loads past it are dropped;
   // a job too large for the image gets an empty range): a fixed count of
   // loads behind wave 0's header loads.
-  {
+  auto bulk_loads = [&]() {
+  if (STG) {
+    if (wv == 0) {  // the loader: the read's first KiB (the head's input), then the part's chunks in order
+      const u32x4s hrs4 = rsrc_words(vb - ibias, jlen + (uint32_t)ibias);
+      dma16_asm<false>(hrs4, 16 * lane, lds_addr(hd.hbuf));
+      const u32x4s irs4 = rsrc_words(vb - ibias + 16 * q_lo, use_img ? 16 * q_n : 0);
+      const uint32_t l0 = lds_addr(img);
+      if constexpr (STG) {
+        constexpr int W = WGCS_GSO_INFLIGHT < kDma ? WGCS_GSO_INFLIGHT : kDma;
+        // the first W image DMAs, then the header's wait (the oldest), then the rest throttled
+#pragma unroll
+        for (int d = 0; d < W; ++d) dma16_asm<NT>(irs4, 16 * (64 * d + lane), l0 + 1024 * d);
+        vm_wait<W>();
+        if (lane == 0) flag_put((lds_flag_t)&hd.hland, 1);
+#if defined(WGCS_GSO_STAMPS) && WGCS_GSO_STAMPS == 3  // loader: T2 header landed
+        stp[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+        loader_issue<kDma, W, WGCS_GSO_STAGE_DMA, W>(irs4, l0, lane, (lds_flag_t)&hd.landed);
+      }
+    }
+  } else {
     const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(vb - ibias + 16 * q_lo), (short)0, use_img ? 16 * q_n : 0, 0x00020000);
 #pragma unroll
@@ -1455,8 +1606,86 @@ __global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(cons
                                                16 * (q0 + lane), 0, 0, NT ? 2 : 0);
     }
   }
-  // ---- wave 0: the head, while the bulk loads are in flight
-  if (wv == 0) {
+  };
+  // ---- the head wave: the head, while the bulk loads are in flight
+  // publish: this wave writes count / status (part 0) and the LDS copy
+  // the job-constant header sums (as gso_rows_kernel) of a clean job: only
+  // finish_row needs them, so the staged row waves compute them after their
+  // first payload stream (the loads and stores of it do not wait for them)
+  auto head_sums = [&](HeadRes& h) {
+    const bool tcp_s = h.type != GSO_UDP_L4;
+    const uint4 Q = h.Q;
+    const int cs = h.cs, hdr_len = h.hdr_len, ipv = h.ipv;
+    const int x0 = 16 * r;
+    const int vlo = cs + 4, vhi = tcp_s ? cs + 8 : cs + 6;
+    const int ca = (cs + h.co) & 0xFFFF;
+    uint32_t ip_base = 0, l4_base = 0, tflags = 0, id0 = 0, seq0 = 0;
+    if (ipv == 4) {
+      const uint32_t m = byte_bits16(-x0, cs - x0) & ~byte_bits16(2 - x0, 6 - x0) & ~byte_bits16(10 - x0, 12 - x0);
+      ip_base = (uint32_t)ufl((int)bswap16(fold32_16(row16_sum_u32(add4_masked(0u, Q, m, false)))));
+    }
+    uint32_t ml4 = byte_bits16(cs - x0, hdr_len - x0) & ~byte_bits16(ca - x0, ca + 2 - x0) &
+                   ~byte_bits16(vlo - x0, vhi - x0);
+    if (tcp_s) ml4 &= ~byte_bits16(cs + 13 - x0, cs + 14 - x0);
+    const int a_lo = ipv == 4 ? 12 : 8, a_hi = ipv == 4 ? 20 : 40;
+    uint32_t s4 = add4_masked(0u, Q, ml4, false);
+    s4 = add4_masked(s4, Q, byte_bits16(a_lo - x0, a_hi - x0), (cs & 1) != 0);
+    uint32_t t4 = fold32_16(row16_sum_u32(s4));
+    if ((cs & 1) == 0) t4 = bswap16(t4);
+    if (tcp_s) tflags = qbyte(Q, cs + 13);
+    l4_base = (uint32_t)ufl((int)t4) + (tflags & ~0x09u);
+    if (ipv == 4) {
+      const uint32_t b45 = qdw(Q, 1);
+      id0 = ((b45 & 0xFFu) << 8) | ((b45 >> 8) & 0xFFu);
+    }
+    if (tcp_s) seq0 = __builtin_bswap32(qle32(Q, vlo));
+    h.ip_base = ip_base;
+    h.l4_base = l4_base;
+    h.tflags = tflags;
+    h.id0 = id0;
+    h.seq0 = seq0;
+  };
+  // the LDS copy of the head's results and the hready word (the loader and,
+  // unstaged, every wave read it)
+  auto publish_geo = [&](const HeadRes& h) {  // the verdict and geometry (staged: + the hgeo word)
+    if (lane == 0) {
+      hd.clean = h.clean;
+      hd.type = h.type;
+      hd.ipv = h.ipv;
+      hd.hdr_len = h.hdr_len;
+      hd.gso = h.gso;
+      hd.cs = h.cs;
+      hd.co = h.co;
+      hd.plen = h.plen;
+    }
+    if (STG) {
+      asm volatile("" ::: "memory");
+      if (lane == 0) flag_put((lds_flag_t)&hd.hgeo, 1);
+    }
+  };
+  auto head_publish = [&](const HeadRes& h) {  // the sums and Q (staged: + the hready word); unstaged: all
+    if (!STG) publish_geo(h);
+    if (lane == 0) {
+      hd.ip_base = h.ip_base;
+      hd.l4_base = h.l4_base;
+      hd.tflags = h.tflags;
+      hd.id0 = h.id0;
+      hd.seq0 = h.seq0;
+    }
+    if (P > 1 && WGCS_GSO_QLDS) {  // the head's Q (every row of the wave holds it; row 0 publishes)
+      if (lane < 16) hd.q[lane] = h.Q;
+    }
+    if (STG) {  // after every field above (one wave's LDS writes complete in order)
+      asm volatile("" ::: "memory");
+      if (lane == 0) flag_put((lds_flag_t)&hd.hready, 1);
+#if defined(WGCS_GSO_STAMPS) && WGCS_GSO_STAMPS == 3  // head wave: T3 head published
+      stp[3] = __builtin_amdgcn_s_memrealtime();
+#endif
+    }
+  };
+  // The verdict and geometry (and count / status when `publish`); with
+  // `sums` also the job-constant header sums.
+  auto head = [&](const uint4 H0, const uint4 w, bool publish, bool sums) -> HeadRes {
     // the virtio header words become scalars only here, behind the bulk loads
     // (a wave-uniform load's value is otherwise moved into SGPRs at the load,
     // with a vmcnt(0) in front of every bulk load)
@@ -1500,83 +1729,149 @@ __global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(cons
       const int th = (int)((qbyte(Q, cs_s + 12) >> 4) * 4);
       clean = ((cs_s + th) & 0xFFFF) == hdr_s;
     }
-    uint32_t ip_base = 0, l4_base = 0, tflags = 0, id0 = 0, seq0 = 0;
     if (ufl(clean ? 1 : 0)) {
-      if (lane == 0 && part == 0) {  // the checks can only end in the segment count here (gso_rows_kernel)
+      if (publish && lane == 0 && part == 0) {  // the checks can only end in the segment count here (gso_rows_kernel)
         const int nfull_s = (plen_s - hdr_s + gso_s - 1) / gso_s;
         const bool many = nfull_s > (int)max_segs;
         count[jb] = many ? (int)max_segs - 1 : nfull_s;
         status[jb] = many ? WGCS_ERR_TOO_MANY_SEGMENTS : 0;
       }
-      // job-constant header sums (as gso_rows_kernel)
-      const int cs = cs_s, hdr_len = hdr_s, ipv = ipv_s;
-      const int x0 = 16 * r;
-      const int vlo = cs + 4, vhi = tcp_s ? cs + 8 : cs + 6;
-      const int ca = ca_s;
-      if (ipv == 4) {
-        const uint32_t m = byte_bits16(-x0, cs - x0) & ~byte_bits16(2 - x0, 6 - x0) & ~byte_bits16(10 - x0, 12 - x0);
-        ip_base = (uint32_t)ufl((int)bswap16(fold32_16(row16_sum_u32(add4_masked(0u, Q, m, false)))));
+    }
+    HeadRes res = {clean ? 1 : 0, type_s, ipv_s, hdr_s, gso_s, cs_s, co_s, plen_s, 0u, 0u, 0u, 0u, 0u, Q};
+    if (sums && res.clean) head_sums(res);
+    return res;
+  };
+  // the head's results from the LDS copy (after the barrier / the hready word)
+  auto sums_from_lds = [&](HeadRes& h) {
+    h.ip_base = (uint32_t)ufl((int)hd.ip_base);
+    h.l4_base = (uint32_t)ufl((int)hd.l4_base);
+    h.tflags = (uint32_t)ufl((int)hd.tflags);
+    h.id0 = (uint32_t)ufl((int)hd.id0);
+    h.seq0 = (uint32_t)ufl((int)hd.seq0);
+    h.Q = (P > 1 && WGCS_GSO_QLDS) ? hd.q[r] : make_uint4(0, 0, 0, 0);
+  };
+  auto head_from_lds = [&]() -> HeadRes {
+    HeadRes h;
+    h.clean = ufl(hd.clean);
+    h.type = ufl(hd.type);
+    h.ipv = ufl(hd.ipv);
+    h.hdr_len = ufl(hd.hdr_len);
+    h.gso = ufl(hd.gso);
+    h.cs = ufl(hd.cs);
+    h.co = ufl(hd.co);
+    h.plen = ufl(hd.plen);
+    h.ip_base = (uint32_t)ufl((int)hd.ip_base);
+    h.l4_base = (uint32_t)ufl((int)hd.l4_base);
+    h.tflags = (uint32_t)ufl((int)hd.tflags);
+    h.id0 = (uint32_t)ufl((int)hd.id0);
+    h.seq0 = (uint32_t)ufl((int)hd.seq0);
+    h.Q = (P > 1 && WGCS_GSO_QLDS) ? hd.q[r] : make_uint4(0, 0, 0, 0);
+    return h;
+  };
+  HeadRes hr = {};
+  if (STG) {  // the loader's DMA; the head wave's loads and head in ONE branch (waited inside it)
+    // the two LDS words start at 0 before any wave may poll them (the
+    // barrier waits on LDS and scalar loads only: the job descriptor)
+    if (threadIdx.x == 0) {
+      flag_put((lds_flag_t)&hd.landed, 0);
+      flag_put((lds_flag_t)&hd.hready, 0);
+      flag_put((lds_flag_t)&hd.hland, 0);
+      flag_put((lds_flag_t)&hd.hgeo, 0);
+    }
+    lds_barrier();
+#if defined(WGCS_GSO_STAMPS) && WGCS_GSO_STAMPS == 3  // per role: T1 past the init barrier
+    stp[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (wv == 0) {
+      bulk_loads();
+    } else {
+      // every row wave runs the head itself from the header bytes (no wait
+      // for one head wave, no LDS round trip); the head wave also publishes
+      // it for the loader
+      if (wv == kHeadWave) {
+        // the verdict and geometry first (the other row waves start their
+        // payload streams on them), then the header sums and Q, which only
+        // finish_row needs
+        HeadIn hi = head_loads();
+#ifdef WGCS_GSO_HEAD_TWICE  // timing-only build: the fast head run twice (is the first run instruction-fetch bound?)
+        hr = head(hi.H0, hi.w, false, false);
+        stp[2] = __builtin_amdgcn_s_memrealtime();
+        asm volatile("" : "+v"(hi.H0.x), "+v"(hi.w.x), "+v"(hi.w.y));
+        if (ufl(hr.gso) == 0x7FFFFFFF) hi.w.x = 0;
+#endif
+        hr = head(hi.H0, hi.w, true, false);
+        publish_geo(hr);
+        if (hr.clean) head_sums(hr);
+        head_publish(hr);
+      } else {
+        while (ufl(flag_get((lds_flag_t)&hd.hgeo)) == 0) __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+        hr = head_from_lds();  // the sums and Q in it are read again once hready is set (ensure_sums)
       }
-      uint32_t ml4 = byte_bits16(cs - x0, hdr_len - x0) & ~byte_bits16(ca - x0, ca + 2 - x0) &
-                     ~byte_bits16(vlo - x0, vhi - x0);
-      if (tcp_s) ml4 &= ~byte_bits16(cs + 13 - x0, cs + 14 - x0);
-      const int a_lo = ipv == 4 ? 12 : 8, a_hi = ipv == 4 ? 20 : 40;
-      uint32_t s4 = add4_masked(0u, Q, ml4, false);
-      s4 = add4_masked(s4, Q, byte_bits16(a_lo - x0, a_hi - x0), (cs & 1) != 0);
-      uint32_t t4 = fold32_16(row16_sum_u32(s4));
-      if ((cs & 1) == 0) t4 = bswap16(t4);
-      if (tcp_s) tflags = qbyte(Q, cs + 13);
-      l4_base = (uint32_t)ufl((int)t4) + (tflags & ~0x09u);
-      if (ipv == 4) {
-        const uint32_t b45 = qdw(Q, 1);
-        id0 = ((b45 & 0xFFu) << 8) | ((b45 >> 8) & 0xFFu);
-      }
-      if (tcp_s) seq0 = __builtin_bswap32(qle32(Q, vlo));
     }
-    if (lane == 0) {
-      hd.clean = clean ? 1 : 0;
-      hd.type = type_s;
-      hd.ipv = ipv_s;
-      hd.hdr_len = hdr_s;
-      hd.gso = gso_s;
-      hd.cs = cs_s;
-      hd.co = co_s;
-      hd.plen = plen_s;
-      hd.ip_base = ip_base;
-      hd.l4_base = l4_base;
-      hd.tflags = tflags;
-      hd.id0 = id0;
-      hd.seq0 = seq0;
-    }
-    if (P > 1 && WGCS_GSO_QLDS) {  // the head's Q (every row of wave 0 holds it; row 0 publishes)
-      if (lane < 16) hd.q[lane] = Q;
-    }
+  } else {
+    HeadIn hi = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    if (wv == kHeadWave) hi = head_loads();
+    __builtin_amdgcn_sched_barrier(0);  // keep the header loads ahead of the bulk loads
+    bulk_loads();
+    if (wv == kHeadWave) head_publish(head(hi.H0, hi.w, true, true));
   }
 #ifdef WGCS_GSO_STAMPS
-  stp[1] = __builtin_amdgcn_s_memrealtime();
+  if (WGCS_GSO_STAMPS != 3) stp[1] = __builtin_amdgcn_s_memrealtime();
 #endif
   // ---- every wave's bulk loads have landed (the compiler's own s_waitcnt,
   // not inline asm: its wait-count pass then knows no LDS-DMA is pending and
   // puts no vmcnt(0) -- which would also wait for the row's earlier stores --
   // in front of the image reads of the row loop); the barrier publishes the
   // image and the head
-  __builtin_amdgcn_s_waitcnt(kVmcnt0);
-  lds_barrier();
-#ifdef WGCS_GSO_STAMPS
-  stp[2] = __builtin_amdgcn_s_memrealtime();
+  const lds_flag_t landed = (lds_flag_t)&hd.landed;
+  if (STG) {
+    // no barrier: the loader publishes its stages while the head wave still
+    // works; every wave but the head wave waits for the head's word
+    if constexpr (STG) {
+      if (wv == 0) {  // the last W instructions' stages (the loader issued every DMA already)
+        constexpr int W = WGCS_GSO_INFLIGHT < kDma ? WGCS_GSO_INFLIGHT : kDma;
+        constexpr int D = WGCS_GSO_STAGE_DMA;
+        publish_stages<kDma, D, (kDma - W) / D * D>(landed, lane);  // ends at vmcnt(0)
+#if defined(WGCS_GSO_STAMPS) && WGCS_GSO_STAMPS == 3  // loader: T3 all landed
+        stp[3] = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (ufl(hd.clean)) {
-    const int type = ufl(hd.type), ipv = ufl(hd.ipv), hdr_len = ufl(hd.hdr_len), gso = ufl(hd.gso);
-    const int cs = ufl(hd.cs), co = ufl(hd.co), plen = ufl(hd.plen);
-    const uint32_t ip_base = (uint32_t)ufl((int)hd.ip_base), l4_base = (uint32_t)ufl((int)hd.l4_base);
-    const uint32_t tflags = (uint32_t)ufl((int)hd.tflags), id0 = (uint32_t)ufl((int)hd.id0);
-    const uint32_t seq0 = (uint32_t)ufl((int)hd.seq0);
+      }
+    }
+    if (wv == 0) {  // the loader takes the head wave's copy
+      while (ufl(flag_get((lds_flag_t)&hd.hready)) == 0) __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+      hr = head_from_lds();
+    }
+#if defined(WGCS_GSO_STAMPS) && WGCS_GSO_STAMPS == 3  // row waves: T2 head computed
+    if (wv > 1) stp[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef WGCS_GSO_STAMPS  // staged: T1 head known, T2 the wave's first rows may start (loader: all landed)
+    if (WGCS_GSO_STAMPS != 3) stp[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+  } else {
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    lds_barrier();
+    hr = head_from_lds();
+  }
+#ifdef WGCS_GSO_STAMPS
+  if (WGCS_GSO_STAMPS != 3) stp[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+  if (ufl(hr.clean)) {
+    const int type = ufl(hr.type), ipv = ufl(hr.ipv), hdr_len = ufl(hr.hdr_len), gso = ufl(hr.gso);
+    const int cs = ufl(hr.cs), co = ufl(hr.co), plen = ufl(hr.plen);
+    // staged: the head wave computes the header sums now and publishes the
+    // head for the loader; the other row waves after their first payload stream
+    bool sums = !STG || wv == 0 || wv == kHeadWave;
+    uint32_t ip_base = (uint32_t)ufl((int)hr.ip_base), l4_base = (uint32_t)ufl((int)hr.l4_base);
+    uint32_t tflags = (uint32_t)ufl((int)hr.tflags), id0 = (uint32_t)ufl((int)hr.id0);
+    uint32_t seq0 = (uint32_t)ufl((int)hr.seq0);
     auto has_seg = [&](int i) { return i < (int)max_segs && hdr_len + (int64_t)i * gso < plen; };
     // readBuf[16r, 16r + 16): from the image, or (a job too large for it)
     // from HBM as gso_rows_kernel reads it
     uint4 Q;
-    if (P > 1 && WGCS_GSO_QLDS) {  // published by wave 0
-      Q = hd.q[r];
+    if (P > 1 && WGCS_GSO_QLDS) {  // the wave's own head (staged) or the head wave's LDS copy
+      Q = hr.Q;
     } else if (P > 1) {  // from the header loads every wave issued first
       const uint32_t nx = row_next(H0.x);
       Q = make_uint4(__builtin_amdgcn_alignbyte(H0.y, H0.x, hph), __builtin_amdgcn_alignbyte(H0.z, H0.y, hph),
@@ -1593,6 +1888,20 @@ __global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(cons
       Q = make_uint4(__builtin_amdgcn_alignbyte(Hq.y, Hq.x, hph), __builtin_amdgcn_alignbyte(Hq.z, Hq.y, hph),
                      __builtin_amdgcn_alignbyte(Hq.w, Hq.z, hph), __builtin_amdgcn_alignbyte(nx, Hq.w, hph));
     }
+    auto ensure_sums = [&]() {
+      if (STG && !sums) {
+        while (ufl(flag_get((lds_flag_t)&hd.hready)) == 0) __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+        sums_from_lds(hr);
+        Q = hr.Q;
+        ip_base = (uint32_t)ufl((int)hr.ip_base);
+        l4_base = (uint32_t)ufl((int)hr.l4_base);
+        tflags = (uint32_t)ufl((int)hr.tflags);
+        id0 = (uint32_t)ufl((int)hr.id0);
+        seq0 = (uint32_t)ufl((int)hr.seq0);
+        sums = true;
+      }
+    };
     // write-through stores through a resource over the job's output region
     // when every row offset fits it (block-uniform; else plain stores)
     // (based at out + obase rounded down to 16 bytes: every row's dbase lies
@@ -1605,11 +1914,35 @@ __global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(cons
     int i0 = 0, i1 = 0x7FFFFFFF;
     if (P > 1) {
       const int64_t a = (int64_t)part * H - 10 - hdr_len, b = a + H;
-      i0 = a <= 0 ? 0 : (int)min((a + gso - 1) / gso, (int64_t)0x7FFFFFFF);
-      if (part < P - 1) i1 = b <= 0 ? 0 : (int)min((b + gso - 1) / gso, (int64_t)0x7FFFFFFF);
+      // ceil(x / gso) in 32 bits where x fits (every read the image holds): a
+      // 64-bit division is a long serial chain on this critical path
+      auto cdiv = [&](int64_t x) -> int {
+        if (x <= 0) return 0;
+        if (x < 0x40000000) return (int)(((uint32_t)x + (uint32_t)gso - 1u) / (uint32_t)gso);
+        return (int)min((x + gso - 1) / gso, (int64_t)0x7FFFFFFF);
+      };
+      i0 = cdiv(a);
+      if (part < P - 1) i1 = cdiv(b);
     }
     const int lo_b = 16 * q_lo - ibias, hi_b = 16 * (q_lo + q_n) - ibias;  // staged job bytes
-    for (int i = i0 + wv * 4 + (lane >> 4); i < i1 && has_seg(i); i += ROWS) {  // row-uniform
+    // staged: the loader (wave 0) takes the last rows of a pass, the other
+    // waves the first ones in order, so they start on the stages that land first
+    // (the head wave, which computes the sums first, takes the rows before the loader's)
+    const int slotw = (STG ? (wv == 0 ? NW - 1 : wv == kHeadWave ? NW - 2 : wv - 2) : wv) * 4;
+    for (int i = i0 + slotw + (lane >> 4); i < i1 && has_seg(i); i += ROWS) {  // row-uniform
+      if (STG && use_img) {
+        // every payload byte of the wave's rows landed: job bytes up to the
+        // end of its last row's segment (+ the window's next dword), image
+        // offset ib_p + x, in loader instructions of 1 KiB
+        const int il = min(ufl(i - (lane >> 4)) + 3, i1 - 1);
+        const int64_t se = min((int64_t)plen, (int64_t)hdr_len + (int64_t)(il + 1) * gso);
+        const int need = ufl((int)min((int64_t)kDma, ((int64_t)ib_p + 10 + se + 4 + 1023) >> 10));
+        while (ufl(flag_get(landed)) < need) __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+#ifdef WGCS_GSO_STAMPS
+        if (wv != 0 && i - (lane >> 4) == i0 + slotw) stp[WGCS_GSO_STAMPS == 3 ? 3 : 2] = __builtin_amdgcn_s_memrealtime();
+#endif
+      }
       uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
       const int dalign = (int)((uintptr_t)dst & 15u);
       uint8_t* dbase = dst - dalign;
@@ -1620,29 +1953,32 @@ __global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(cons
         in_img = g.lo - 18 >= lo_b && (g.hi + 20 <= hi_b || q_lo + q_n >= nch) &&
                  ib_p + g.aoff + 16 * ((g.nk + 16 * U - 1) / (16 * U) * 16 * U) + 4 <= kArr;
       }
+      RowOut ro;
+      ro.keep = make_uint4(0, 0, 0, 0);
+      ro.rs = ors;
+      ro.dro = (int)(dbase - obase16);
+      ro.wt = wt;
       if (in_img) {
-        RowOut ro;
-        ro.keep = make_uint4(0, 0, 0, 0);
-        ro.rs = ors;
-        ro.dro = (int)(dbase - obase16);
-        ro.wt = wt;
 #ifndef WGCS_GSO_PROBE_NOSTREAM  // timing-only builds (not exact output): the row's parts alone
         stream_row_img<U>(img, ib_p, rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, ro);
 #endif
-#ifndef WGCS_GSO_PROBE_NOFINISH
-        finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
-                   tflags, id0, seq0, &sizes[slot0 + (uint32_t)i], &ro);
-#else
-        if (r == 0) sizes[slot0 + (uint32_t)i] = (int32_t)acc;
-#endif
       } else {
         stream_row<U, NT>(rb, i, gso, hdr_len, plen, dalign, dbase, r, acc, job_rsrc(vb, jlen));
+      }
+      ensure_sums();  // one place: the header sums' code is inlined once
+#ifndef WGCS_GSO_PROBE_NOFINISH
+      if (in_img)
+        finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
+                   tflags, id0, seq0, &sizes[slot0 + (uint32_t)i], &ro);
+      else
         finish_row(true, Q, type, ipv, hdr_len, gso, cs, co, plen, i, r, dalign, dst, dbase, acc, ip_base, l4_base,
                    tflags, id0, seq0, &sizes[slot0 + (uint32_t)i]);
-      }
+#else
+      if (r == 0) sizes[slot0 + (uint32_t)i] = (int32_t)acc;
+#endif
     }
 #ifdef WGCS_GSO_STAMPS
-    stp[3] = __builtin_amdgcn_s_memrealtime();
+    if (WGCS_GSO_STAMPS != 3) stp[3] = __builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stp[4] = __builtin_amdgcn_s_memrealtime();
     if (lane == 0 && max_segs >= 128 && part * NW + wv < 12) {
