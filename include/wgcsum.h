@@ -268,6 +268,33 @@ int wgcs_gso_split_cap(wgcs_ctx *ctx, uint8_t *read_buf, size_t len, size_t cap,
 int wgcs_handle_gro(wgcs_ctx *ctx, uint8_t **bufs, size_t *lens, size_t *caps, int n,
                     int offset, int can_udp_gro, int *to_write, int *n_to_write);
 
+/* ---- the resident per-call ring (round 6) ----
+ * The per-call forms above pay one kernel launch plus one completion wait per
+ * Go call (~20 us).  A ring keeps a small kernel resident on a few CUs of its
+ * own stream: a call writes a request record in fine-grained pinned host
+ * memory and spins on a completion word the kernel bumps, so one Tun.Read /
+ * checksumValid costs a PCIe round trip instead of a launch.  Same arguments,
+ * bytes and errors as wgcs_checksum_valid[_cap] / wgcs_handle_virtio_read[_cap]
+ * (tun/gro.go:554-612, tun/tun.go:514-632).  Request bytes in wgcs_host_alloc
+ * memory are read in place; other caller memory is copied into the ring's
+ * staging.  The kernel leaves after idle_us (0: 100 ms) without a request and
+ * a later call launches it again; one call at a time per ring (it locks).
+ * wgcs_ring_destroy stops the kernel and waits for it. */
+typedef struct wgcs_ring wgcs_ring;
+int wgcs_ring_create(wgcs_ctx *ctx, uint32_t idle_us, wgcs_ring **out);
+int wgcs_ring_destroy(wgcs_ring *ring);
+/* requests served, kernel launches made, 1 while the kernel is resident */
+int wgcs_ring_info(wgcs_ring *ring, uint64_t *requests, uint64_t *launches, int *running);
+int wgcs_ring_checksum_valid(wgcs_ring *ring, const uint8_t *pkt, size_t len, uint8_t iph_len, uint8_t proto,
+                             int is_v6, int *valid);
+int wgcs_ring_checksum_valid_cap(wgcs_ring *ring, const uint8_t *pkt, size_t len, size_t cap, uint8_t iph_len,
+                                 uint8_t proto, int is_v6, int *valid);
+int wgcs_ring_handle_virtio_read(wgcs_ring *ring, uint8_t *read_buf, size_t n, uint8_t *const *bufs,
+                                 const size_t *buf_lens, int nbufs, int *sizes, int offset, int *n_out);
+int wgcs_ring_handle_virtio_read_cap(wgcs_ring *ring, uint8_t *read_buf, size_t n, size_t cap,
+                                     uint8_t *const *bufs, const size_t *buf_lens, int nbufs, int *sizes,
+                                     int offset, int *n_out);
+
 /* ---- device-resident batch of Tun.Write calls (handleGRO per call) ----
  * bufs[i] of a call is the Go slice d_arena[off : off+len] with cap(bufs[i]) =
  * cap; every slice owns d_arena[off, off+cap), and the arena must be readable

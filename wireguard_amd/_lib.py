@@ -131,6 +131,15 @@ def load() -> C.CDLL:
         "wgcs_wstager_push_pinned": ([vp, C.POINTER(vp), C.POINTER(sz), C.POINTER(sz), i32, i32, i32,
                                       C.POINTER(i32)], i32),
         "wgcs_wstager_submit": ([vp, C.POINTER(u64)], i32),
+        "wgcs_ring_create": ([vp, u32, C.POINTER(vp)], i32),
+        "wgcs_ring_destroy": ([vp], i32),
+        "wgcs_ring_info": ([vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(i32)], i32),
+        "wgcs_ring_checksum_valid": ([vp, vp, sz, C.c_uint8, C.c_uint8, i32, C.POINTER(i32)], i32),
+        "wgcs_ring_checksum_valid_cap": ([vp, vp, sz, sz, C.c_uint8, C.c_uint8, i32, C.POINTER(i32)], i32),
+        "wgcs_ring_handle_virtio_read": ([vp, vp, sz, u8pp, C.POINTER(sz), i32, C.POINTER(i32), i32,
+                                          C.POINTER(i32)], i32),
+        "wgcs_ring_handle_virtio_read_cap": ([vp, vp, sz, sz, u8pp, C.POINTER(sz), i32, C.POINTER(i32), i32,
+                                              C.POINTER(i32)], i32),
         "wgcs_host_alloc": ([vp, sz, C.POINTER(vp)], i32),
         "wgcs_host_free": ([vp, vp], i32),
         "wgcs_stream_wait_flag": ([vp, vp, vp, u32], i32),

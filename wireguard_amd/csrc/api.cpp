@@ -162,7 +162,10 @@ int wgcs_host_alloc(wgcs_ctx* ctx, size_t bytes, void** p) {
   hipSetDevice(ctx->device);
   const size_t n = (bytes + 15) & ~(size_t)15;
   void* h = nullptr;
-  hipError_t e = hipHostMalloc(&h, n, hipHostMallocDefault);
+  // fine-grained (coherent): the resident ring (ring.cpp) reads request bytes
+  // here in place, and a buffer reused at one address between requests must
+  // not be served from a stale GPU cache line
+  hipError_t e = hipHostMalloc(&h, n, hipHostMallocCoherent);
   if (e != hipSuccess) return hip_fail(ctx, e, "wgcs_host_alloc");
   void* d = nullptr;
   e = hipHostGetDevicePointer(&d, h, 0);

@@ -35,8 +35,11 @@ struct GsoResult {
 // The room checks use bufs[0]'s room, as the reference does (tun/tun.go:546,
 // gro.go:1406-1410); other buffers are checked when copying, where the Go
 // code would panic on the slice.  Caller holds ctx->mu.
+// With `ring` the device step goes through the resident ring instead of a
+// launch + wait (its own coherent staging; the caller holds the ring's lock).
 int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflags, uint8_t* const* bufs,
-                 const size_t* buf_lens, int nbufs, int* sizes, int offset, GsoResult* res) {
+                 const size_t* buf_lens, int nbufs, int* sizes, int offset, GsoResult* res,
+                 wgcs_ring* ring = nullptr) {
   if (nbufs < 0 || (nbufs > 0 && (!bufs || !buf_lens || !sizes)) || offset < 0)
     return set_err(ctx, WGCS_ERR_INVALID_ARG, "bufs/sizes/offset");
   if (vlen > 0x7FFFFFF0u) return set_err(ctx, WGCS_ERR_INVALID_ARG, "super-packet too large");
@@ -65,34 +68,52 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
   const size_t region = (size_t)pitch * nseg_bound;
   hipSetDevice(ctx->device);
   int rc;
-  const size_t meta = ((size_t)kbufs * 4 + 16 + 15) & ~(size_t)15;  // sizes[kbufs] | count | status
-  const size_t aux = sizeof(wgcs_gso_job) + sizeof(GsoOutPos);
-  if ((rc = ensure_pinned(ctx, ctx->h_meta, meta + aux)) || (rc = ensure_pinned(ctx, ctx->h_stage, region + 16)))
-    return rc;
-  hipStream_t s = ctx->stream;
-  uint8_t* hm = (uint8_t*)ctx->h_meta.ptr;
-  wgcs_gso_job* hjob = (wgcs_gso_job*)(hm + meta);
-  GsoOutPos* hpos = (GsoOutPos*)(hjob + 1);
-  hjob->off = 0;
-  hjob->len = (uint32_t)vlen;
-  hjob->flags = jflags;
-  hpos->base = 0;
-  hpos->pitch = pitch;
-  hpos->flags = mirror ? kOutPosTails : 0u;
-  int32_t* h = (int32_t*)hm;
-  uint8_t* hs = (uint8_t*)ctx->h_stage.ptr;
-  if (mirror && region) {
-    memset(hs, 0, region);
-    for (uint32_t i = 0; i < nseg_bound && i < (uint32_t)nbufs; ++i)
-      if (buf_lens[i] > (size_t)offset)
-        memcpy(hs + (size_t)i * pitch, bufs[i] + offset, std::min<size_t>(pitch, buf_lens[i] - offset));
+  int32_t* h;
+  uint8_t* hs;
+  auto stage_mirror = [&]() {
+    if (mirror && region) {
+      memset(hs, 0, region);
+      for (uint32_t i = 0; i < nseg_bound && i < (uint32_t)nbufs; ++i)
+        if (buf_lens[i] > (size_t)offset)
+          memcpy(hs + (size_t)i * pitch, bufs[i] + offset, std::min<size_t>(pitch, buf_lens[i] - offset));
+    }
+  };
+  if (ring) {
+    // the ring stages the mirror itself: its region is known once it has grown
+    uint8_t* rs = nullptr;
+    int32_t* rm = nullptr;
+    if ((rc = ring_gso_prepare(ring, (uint32_t)kbufs, region, &rs, &rm))) return rc;
+    hs = rs;
+    h = rm;
+    stage_mirror();
+    if ((rc = ring_gso(ring, vbuf, (uint32_t)vlen, jflags, (uint32_t)kbufs, pitch, (uint32_t)room,
+                       mirror ? kOutPosTails : 0u, region, &rs, &rm)))
+      return rc;
+  } else {
+    const size_t meta = ((size_t)kbufs * 4 + 16 + 15) & ~(size_t)15;  // sizes[kbufs] | count | status
+    const size_t aux = sizeof(wgcs_gso_job) + sizeof(GsoOutPos);
+    if ((rc = ensure_pinned(ctx, ctx->h_meta, meta + aux)) || (rc = ensure_pinned(ctx, ctx->h_stage, region + 16)))
+      return rc;
+    hipStream_t s = ctx->stream;
+    uint8_t* hm = (uint8_t*)ctx->h_meta.ptr;
+    wgcs_gso_job* hjob = (wgcs_gso_job*)(hm + meta);
+    GsoOutPos* hpos = (GsoOutPos*)(hjob + 1);
+    hjob->off = 0;
+    hjob->len = (uint32_t)vlen;
+    hjob->flags = jflags;
+    hpos->base = 0;
+    hpos->pitch = pitch;
+    hpos->flags = mirror ? kOutPosTails : 0u;
+    h = (int32_t*)hm;
+    hs = (uint8_t*)ctx->h_stage.ptr;
+    stage_mirror();
+    // pinned staging is mapped into the device's address space at its host
+    // address (checked by ensure_pinned's hipHostMalloc contract, see api.cpp)
+    hipError_t e = launch_gso_split_batch(vbuf, hjob, 1, hs, 0, 0, (uint32_t)kbufs, h, h + kbufs, h + kbufs + 1, s,
+                                          hpos, (uint32_t)room);
+    if (e != hipSuccess) return hip_fail(ctx, e, "gso_split launch");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "gso_split wait");
   }
-  // pinned staging is mapped into the device's address space at its host
-  // address (checked by ensure_pinned's hipHostMalloc contract, see api.cpp)
-  hipError_t e = launch_gso_split_batch(vbuf, hjob, 1, hs, 0, 0, (uint32_t)kbufs, h, h + kbufs, h + kbufs + 1, s,
-                                        hpos, (uint32_t)room);
-  if (e != hipSuccess) return hip_fail(ctx, e, "gso_split launch");
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "gso_split wait");
   res->count = h[kbufs];
   res->status = h[kbufs + 1];
   if (nobuf) {
@@ -125,6 +146,28 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
     memcpy(bufs[i] + offset, hs + (size_t)i * pitch, mirror ? need : (size_t)h[i]);
   }
   return WGCS_OK;
+}
+
+// handleVirtioRead's edits of the caller's readBuf after a split (the GPU
+// worked on a copy or read it in place without writing it).
+void finish_virtio_read(uint8_t* read_buf, size_t n, uint8_t* const* bufs, int offset, const GsoResult& r) {
+  if (n >= 10 && (r.status == 0 || r.status == WGCS_ERR_TOO_MANY_SEGMENTS)) {
+    uint8_t* rb = read_buf + 10;
+    uint16_t cs, co;
+    memcpy(&cs, read_buf + 6, 2);
+    memcpy(&co, read_buf + 8, 2);
+    const size_t at = (uint16_t)(cs + co);
+    if (read_buf[1] == 0) {
+      // GSO_NONE: gsoNoneChecksum wrote the checksum into readBuf (gro.go:1512-1515)
+      if (read_buf[0] & 1) {
+        rb[at] = bufs[0][offset + at];
+        rb[at + 1] = bufs[0][offset + at + 1];
+      }
+    } else {
+      if ((rb[0] >> 4) == 4) rb[10] = rb[11] = 0;  // gro.go:1388
+      rb[at] = rb[at + 1] = 0;                     // gro.go:1393
+    }
+  }
 }
 
 }  // namespace
@@ -222,23 +265,7 @@ int wgcs_handle_virtio_read_cap(wgcs_ctx* ctx, uint8_t* read_buf, size_t n, size
   rc = run_gso_host(ctx, (const uint8_t*)ctx->h_out.ptr, n, WGCS_GSO_JOB_SPARE(spare), bufs, buf_lens, nbufs, sizes,
                     offset, &r);
   if (rc) return rc;
-  if (n >= 10 && (r.status == 0 || r.status == WGCS_ERR_TOO_MANY_SEGMENTS)) {
-    uint8_t* rb = read_buf + 10;
-    uint16_t cs, co;
-    memcpy(&cs, read_buf + 6, 2);
-    memcpy(&co, read_buf + 8, 2);
-    const size_t at = (uint16_t)(cs + co);
-    if (read_buf[1] == 0) {
-      // GSO_NONE: gsoNoneChecksum wrote the checksum into readBuf (gro.go:1512-1515)
-      if (read_buf[0] & 1) {
-        rb[at] = bufs[0][offset + at];
-        rb[at + 1] = bufs[0][offset + at + 1];
-      }
-    } else {
-      if ((rb[0] >> 4) == 4) rb[10] = rb[11] = 0;  // gro.go:1388
-      rb[at] = rb[at + 1] = 0;                     // gro.go:1393
-    }
-  }
+  finish_virtio_read(read_buf, n, bufs, offset, r);
   *n_out = r.count;
   return r.status;
 }
@@ -246,6 +273,31 @@ int wgcs_handle_virtio_read_cap(wgcs_ctx* ctx, uint8_t* read_buf, size_t n, size
 int wgcs_handle_virtio_read(wgcs_ctx* ctx, uint8_t* read_buf, size_t n, uint8_t* const* bufs, const size_t* buf_lens,
                             int nbufs, int* sizes, int offset, int* n_out) {
   return wgcs_handle_virtio_read_cap(ctx, read_buf, n, n, bufs, buf_lens, nbufs, sizes, offset, n_out);
+}
+
+// handleVirtioRead through the resident ring (ring.cpp): the same arguments,
+// bytes and errors as wgcs_handle_virtio_read_cap.
+int wgcs_ring_handle_virtio_read_cap(wgcs_ring* ring, uint8_t* read_buf, size_t n, size_t cap, uint8_t* const* bufs,
+                                     const size_t* buf_lens, int nbufs, int* sizes, int offset, int* n_out) {
+  if (!ring || !n_out || (!read_buf && cap) || cap < n) return WGCS_ERR_INVALID_ARG;
+  *n_out = 0;
+  wgcs_ctx* ctx = ring_ctx(ring);
+  const size_t spare = std::min<size_t>(cap - n, 255);
+  GsoResult r;
+  std::lock_guard<std::mutex> g(ring_mutex(ring));
+  const uint8_t* vbuf = nullptr;
+  int rc = ring_input(ring, read_buf, n + spare, &vbuf);
+  if (rc) return rc;
+  rc = run_gso_host(ctx, vbuf, n, WGCS_GSO_JOB_SPARE(spare), bufs, buf_lens, nbufs, sizes, offset, &r, ring);
+  if (rc) return rc;
+  finish_virtio_read(read_buf, n, bufs, offset, r);
+  *n_out = r.count;
+  return r.status;
+}
+
+int wgcs_ring_handle_virtio_read(wgcs_ring* ring, uint8_t* read_buf, size_t n, uint8_t* const* bufs,
+                                 const size_t* buf_lens, int nbufs, int* sizes, int offset, int* n_out) {
+  return wgcs_ring_handle_virtio_read_cap(ring, read_buf, n, n, bufs, buf_lens, nbufs, sizes, offset, n_out);
 }
 
 }  // extern "C"

@@ -1008,13 +1008,15 @@ __device__ __noinline__ int decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, u
 #ifndef WGCS_GSO_GROUPS
 #define WGCS_GSO_GROUPS 3  // blocks per job (grid y); each takes every WGCS_GSO_GROUPS-th segment group
 #endif
+// One (job, segment-group set) of gso_rows_kernel: block `by` of `gy` blocks
+// per job takes the job's segment groups by, by + gy, ...  The descriptor and
+// output position come by value (the resident ring kernel passes a request's,
+// gso_rows_kernel its grid's); `has_pos`: use pos, else fixed slots.
 template <int U, bool NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WAVES, 8))) void gso_rows_kernel(const uint8_t* __restrict__ arena,
-                                                       const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
-                                                       uint8_t* __restrict__ out, uint32_t out_stride,
-                                                       const GsoOutPos* __restrict__ outpos, uint32_t offset,
-                                                       uint32_t room, int32_t* __restrict__ sizes,
-                                                       int32_t* __restrict__ count, int32_t* __restrict__ status) {
+__device__ __forceinline__ void gso_rows_body(const uint8_t* arena, const wgcs_gso_job job, uint32_t jb, int by,
+                                              int gy, uint32_t max_segs, uint8_t* out, uint32_t out_stride,
+                                              bool has_pos, const GsoOutPos pos, uint32_t offset, uint32_t room,
+                                              int32_t* sizes, int32_t* count, int32_t* status) {
   constexpr int ROWS = 16;
 #ifdef WGCS_GSO_STAMPS  // timing-only build (scripts/probe_gso_stamps.py): s_memrealtime per wave phase
   uint64_t stp[5] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0};
@@ -1022,8 +1024,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   const int lane = threadIdx.x & 63;
   const int r = lane & 15;
   const int wv = threadIdx.x >> 6;
-  const uint32_t jb = blockIdx.x;
-  const wgcs_gso_job job = jobs[jb];  // one scalar load of the whole descriptor, flags included
   const uint8_t* vb = arena + job.off;
   const uint32_t jlen = job.len;
   const uint8_t* rb = vb + 10;
@@ -1033,10 +1033,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   uint64_t obase = slot0 * out_stride;
   uint32_t opitch = out_stride;
   uint32_t tails = 1;  // gsoSplit's header writes past a segment's end (GsoOutPos)
-  if (outpos) {
-    obase = outpos[jb].base;
-    opitch = outpos[jb].pitch;
-    tails = outpos[jb].flags & kOutPosTails;
+  if (has_pos) {
+    obase = pos.base;
+    opitch = pos.pitch;
+    tails = pos.flags & kOutPosTails;
   }
   // ---- header chunks in packet coordinates (lane r of each row: the
   // dword-aligned 16-byte window r from the dword holding readBuf[0]; shifted
@@ -1058,8 +1058,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   uint32_t t1 = 0, hl = 0, g = 0, c = 0, o = 0, b0 = 0;
   if (jlen >= 14) {
     const int sh = (int)((uintptr_t)vb & 3u);
-    typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-    const u32x4a4 w = *reinterpret_cast<const u32x4a4*>(__builtin_assume_aligned(vb - sh, 4));
+    // a range-checked vector load (zeros past the job), not a scalar one: the
+    // resident ring kernel reads requests that change at the same address
+    const uint4 w = bld16<false>(__builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vb - sh), (short)0,
+                                                                 (int)(jlen + 3u + (uint32_t)sh), 0x00020000), 0);
     const uint64_t lo = ((uint64_t)w.y << 32) | w.x, hi = ((uint64_t)w.w << 32) | w.z;
     // bytes [sh, sh + 11) of the 16: the virtio header and readBuf[0]
     const uint64_t v0 = sh ? (lo >> (8 * sh)) | (hi << (64 - 8 * sh)) : lo;  // vb[0..8)
@@ -1108,10 +1110,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
     if (gso_none || y >= ngroups) return false;
     return !split_type || (plen_s > hmin && hmin + (int64_t)y * ROWS * gso_s < plen_s);
   };
-  if (!group_live((int)blockIdx.y)) return;
+  if (!group_live(by)) return;
 #ifdef WGCS_GSO_HEAD_MIN  // timing-only build: descriptor + virtio header + verdict inputs, nothing else
-  if (threadIdx.x == 0 && blockIdx.y == 0) count[jb] = ok_s ? 45 : 0;
-  if (threadIdx.x == 0 && blockIdx.y == 0) status[jb] = clean_s ? 0 : 1;
+  if (threadIdx.x == 0 && by == 0) count[jb] = ok_s ? 45 : 0;
+  if (threadIdx.x == 0 && by == 0) status[jb] = clean_s ? 0 : 1;
   return;
 #endif
 
@@ -1133,7 +1135,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
   // stay its own (the verdict waits on the header chunks, which arrive with
   // the virtio header).  readfirstlane makes the branch provably uniform.
   if (ufl(clean ? 1 : 0)) {
-    if (blockIdx.y == 0 && threadIdx.x == 0) {  // the checks can only end in the segment count here
+    if (by == 0 && threadIdx.x == 0) {  // the checks can only end in the segment count here
       const int nfull_s = (plen_s - hdr_s + gso_s - 1) / gso_s;
       const bool many = nfull_s > (int)max_segs;
       count[jb] = many ? (int)max_segs - 1 : nfull_s;
@@ -1180,7 +1182,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
     if (ufl((int)(ip_base + l4_base + tflags + id0 + seq0)) == 0x7FFFFFFF) sizes[slot0] = 0;
     return;
 #endif
-    for (int grp = (int)blockIdx.y; has_seg(grp * ROWS); grp += (int)gridDim.y) {  // block-uniform
+    for (int grp = by; has_seg(grp * ROWS); grp += gy) {  // block-uniform
       const int i = grp * ROWS + wv * 4 + (lane >> 4);  // this row's segment
       if (has_seg(i)) {  // row-uniform
         uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
@@ -1203,12 +1205,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stp[4] = __builtin_amdgcn_s_memrealtime();
     if (lane == 0 && max_segs >= 128) {
-      int32_t* sp = sizes + slot0 + 64 + (blockIdx.y * 4 + wv) * 5;
+      int32_t* sp = sizes + slot0 + 64 + (by * 4 + wv) * 5;
       for (int k = 0; k < 5; ++k) sp[k] = (int32_t)(uint32_t)stp[k];
     }
 #endif
   } else {
-    for (int grp = (int)blockIdx.y; group_live(grp); grp += (int)gridDim.y) {  // block-uniform
+    for (int grp = by; group_live(grp); grp += gy) {  // block-uniform
       const int i = grp * ROWS + wv * 4 + (lane >> 4);
       uint8_t* dst = out + obase + (uint64_t)i * opitch + offset;
       const int live = decoded_rows<U, NT>(vb, jlen, job.flags, room, max_segs, i, grp == 0, &count[jb], &status[jb],
@@ -1216,9 +1218,162 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
       lds_barrier();  // every wave is done with this group's verdict before the next one is published
       // the verdict bounds the job's segments (0 for an error / GSO_NONE): no
       // decode + barrier round for groups past it, whatever max_segs is
-      if ((int64_t)(grp + (int)gridDim.y) * ROWS >= (int64_t)ufl(live)) break;
+      if ((int64_t)(grp + gy) * ROWS >= (int64_t)ufl(live)) break;
     }
   }
+}
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WAVES, 8))) void gso_rows_kernel(const uint8_t* __restrict__ arena,
+                                                       const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
+                                                       uint8_t* __restrict__ out, uint32_t out_stride,
+                                                       const GsoOutPos* __restrict__ outpos, uint32_t offset,
+                                                       uint32_t room, int32_t* __restrict__ sizes,
+                                                       int32_t* __restrict__ count, int32_t* __restrict__ status) {
+  const uint32_t jb = blockIdx.x;
+  const GsoOutPos pos = outpos ? outpos[jb] : GsoOutPos{};
+  gso_rows_body<U, NT>(arena, jobs[jb], jb, (int)blockIdx.y, (int)gridDim.y, max_segs, out, out_stride,
+                       outpos != nullptr, pos, offset, room, sizes, count, status);
+}
+
+// ---------------------------------------------------------------------------
+// The resident per-call ring (round 6).  A launch plus a
+// completion wait costs ~20 us per Go call, more than the Go
+// code of one Tun.Read.  ring_kernel stays resident on a few CUs instead:
+// thread 0 of every workgroup polls the request word in coherent pinned host
+// memory (system-scope loads, s_sleep between polls), the workgroups run the
+// request -- checksumValid of one packet (workgroup 0's first wave) or one
+// handleVirtioRead (gso_rows_body: workgroup b takes segment groups b, b + nb,
+// ...) -- reading the request bytes from coherent host memory and writing the
+// results there, then each workgroup releases its stores at system scope and
+// adds 1 to the completion word the host spins on.  Every wave leaves the
+// loop on the stop word or when no request came for `idle_ticks` of
+// s_memrealtime (100 MHz), so no launch can outlive its use.
+
+__device__ __forceinline__ uint32_t ld_sys32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// checksumValid(pkt, iphLen, proto, isV6) (gro.go:554-612) by one wave: the
+// batch kernel's VALIDATE arithmetic (checksum_kernels.hip) over every chunk
+// with byte masks -- the main range pkt[iphLen:len] paired from iphLen, the
+// pseudo-header addresses paired from their own start (rotl8 when the two
+// parities differ) -- then proto + (len - iphLen).  Loads are system-scope
+// (sc0 sc1) buffer loads: the bytes change between requests at one address.
+__device__ uint32_t ring_validate(const uint8_t* pkt, int len, int cs, int proto, bool v6) {
+  const int lane = threadIdx.x & 63;
+  const int main_lo = min(cs, len), main_hi = len;
+  const int addr_lo = v6 ? 8 : 12, addr_hi = v6 ? 40 : 20;
+  const uintptr_t pbase = (uintptr_t)pkt;
+  const bool rot_addr = (((pbase + (uintptr_t)addr_lo) ^ (pbase + (uintptr_t)main_lo)) & 1u) != 0;
+  const int lo_all = min(main_lo, addr_lo), hi_all = max(main_hi, addr_hi);
+  const int rel0 = lo_all - (int)((pbase + (uintptr_t)lo_all) & 15u);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pkt + rel0), (short)0,
+                                                                      hi_all - rel0, 0x00020000);
+  uint32_t acc = 0;
+  for (int c = lane; rel0 + 16 * c < hi_all; c += 64) {
+    const int pos = rel0 + 16 * c;
+    const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * c, 0, 17);
+    const uint32_t w[4] = {t[0], t[1], t[2], t[3]};
+    const uint32_t m16 = byte_bits16(main_lo - pos, main_hi - pos);
+    const uint32_t a16 = byte_bits16(addr_lo - pos, addr_hi - pos);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc = add_halves(acc, w[k] & expand_nibble((m16 >> (4 * k)) & 0xFu));
+      uint32_t y = w[k] & expand_nibble((a16 >> (4 * k)) & 0xFu);
+      if (rot_addr) y = rotl8(y);
+      acc = add_halves(acc, y);
+    }
+    acc = (acc >> 16) + (acc & 0xFFFFu);
+  }
+  uint32_t s = fold32_16(wave_sum_u32(fold32_16(acc)));
+  if (((pbase + (uintptr_t)main_lo) & 1u) == 0) s = bswap16(s);
+  const uint32_t t = fold32_16(s + (uint32_t)proto + ((uint32_t)(len - cs) & 0xFFFFu));
+  return (t == 0xFFFFu && cs <= len) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0, uint64_t idle_ticks) {
+  __shared__ uint32_t s_q;
+  __shared__ RingReq s_r;
+  RingReq* const rq = &ctl->req;
+  uint32_t last = last0;
+  uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint32_t q;
+      for (;;) {
+        q = ld_sys32(&rq->seq);
+        if (ld_sys32(&rq->stop)) {
+          q = 0xFFFFFFFFu;
+          break;
+        }
+        if (q != last) break;
+        if (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
+          q = 0xFFFFFFFFu;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      s_q = q;
+      if (q != 0xFFFFFFFFu) {  // the request's fields, stored by the host before seq
+        s_r.op = ld_sys32(&rq->op);
+        s_r.pkt = ld_sys64(&rq->pkt);
+        s_r.len = ld_sys32(&rq->len);
+        s_r.cs = ld_sys32(&rq->cs);
+        s_r.proto = ld_sys32(&rq->proto);
+        s_r.flags = ld_sys32(&rq->flags);
+        s_r.vbuf = ld_sys64(&rq->vbuf);
+        s_r.vlen = ld_sys32(&rq->vlen);
+        s_r.jflags = ld_sys32(&rq->jflags);
+        s_r.kbufs = ld_sys32(&rq->kbufs);
+        s_r.pitch = ld_sys32(&rq->pitch);
+        s_r.room = ld_sys32(&rq->room);
+        s_r.posflags = ld_sys32(&rq->posflags);
+        s_r.out = ld_sys64(&rq->out);
+        s_r.meta = ld_sys64(&rq->meta);
+      }
+    }
+    __syncthreads();
+    const uint32_t q = s_q;
+    if (q == 0xFFFFFFFFu) break;  // block-uniform: every wave leaves
+    const uint32_t op = (uint32_t)ufl((int)s_r.op);
+    if (op == kRingOpChecksumValid) {
+      if (blockIdx.x == 0 && threadIdx.x < 64) {
+        const uint32_t v = ring_validate(reinterpret_cast<const uint8_t*>(s_r.pkt), (int)s_r.len, (int)s_r.cs,
+                                         (int)s_r.proto, (s_r.flags & WGCS_PKT_V6) != 0);
+        if (threadIdx.x == 0) __hip_atomic_store(&ctl->dn.valid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    } else if (op == kRingOpVirtioRead) {
+      const wgcs_gso_job job = {0, s_r.vlen, s_r.jflags};
+      const GsoOutPos pos = {0, s_r.pitch, s_r.posflags};
+      int32_t* h = reinterpret_cast<int32_t*>(s_r.meta);
+      const uint32_t kb = s_r.kbufs;
+      gso_rows_body<WGCS_GSO_U, false>(reinterpret_cast<const uint8_t*>(s_r.vbuf), job, 0, (int)blockIdx.x,
+                                       (int)gridDim.x, kb, reinterpret_cast<uint8_t*>(s_r.out), 0, true, pos, 0,
+                                       s_r.room, h, h + kb, h + kb + 1);
+    }
+    // completion: every wave's stores done, then one release at system scope
+    // and the count (the fence's own wait is made explicit: MI355X_MICROARCH.md)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(&ctl->dn.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    last = q;
+    t_last = __builtin_amdgcn_s_memrealtime();
+  }
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(&ctl->dn.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_ring(RingCtl* ctl, uint32_t nb, uint32_t last, uint64_t idle_ticks, hipStream_t s) {
+  if (nb == 0 || nb > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ring_kernel, dim3(nb), dim3(256), 0, s, ctl, last, idle_ticks);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

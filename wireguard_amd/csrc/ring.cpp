@@ -1,0 +1,253 @@
+// ring.cpp -- the resident per-call ring (include/wgcsum.h, wgcs_ring_*).
+//
+// Round 6: the per-call entry points (wgcs_checksum_valid,
+// wgcs_handle_virtio_read) pay one kernel launch plus one completion wait per
+// Go call -- ~20 us on MI355X, more than the Go code of one Tun.Read
+// (INTEGRATION.md §2.0).  A ring keeps ring_kernel
+// (gso_kernels.hip) resident on a few CUs of its own stream; a call fills the
+// request record in fine-grained pinned host memory, publishes it by storing
+// the request number last, and spins on the completion word the workgroups
+// bump after a system-scope release of their results.  Same arguments, bytes
+// and errors as the per-call forms (tun/gro.go:554-612, tun/tun.go:514-632);
+// only the transport differs.
+//
+// Liveness: the kernel leaves after `idle_us` without a request (and on
+// wgcs_ring_destroy's stop word), so no launch outlives its use; a call that
+// finds it gone (hipStreamQuery) launches it again, telling it the request
+// number it last served.  One request is in flight at a time (ring->mu).
+// Memory: the request bytes must be readable as they are at the call -- the
+// ring's own staging and wgcs_host_alloc memory are fine-grained (coherent)
+// allocations the GPU does not cache; other caller memory is copied into the
+// ring's staging first, and results land in the ring's staging and are copied
+// out (gso_api.cpp's post-processing), so every byte matches the per-call path.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <thread>
+
+#include "../../include/wgcsum.h"
+#include "wgcs_ctx.h"
+#include "wgcs_kernels.h"
+
+using namespace wgcs;
+
+struct wgcs_ring {
+  wgcs_ctx* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  RingCtl* ctl = nullptr;     // coherent pinned: the request and completion records
+  uint8_t* in = nullptr;      // coherent pinned: copied request bytes
+  size_t in_cap = 0;
+  uint8_t* stage = nullptr;   // coherent pinned: segments / meta of a handleVirtioRead
+  size_t stage_cap = 0;
+  uint32_t nb = 3;            // workgroups (segment groups of a 64-KiB read: 3 x 16 rows)
+  uint64_t idle_ticks = 0;    // s_memrealtime ticks (100 MHz)
+  uint32_t seq = 0;           // last request number posted
+  uint64_t requests = 0, launches = 0;
+  std::mutex mu;
+};
+
+namespace {
+
+int grow_coherent(wgcs_ctx* ctx, uint8_t** p, size_t* cap, size_t want) {
+  if (want <= *cap) return WGCS_OK;
+  if (*p) hipHostFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  const size_t n = ((want < 65536 ? 65536 : want + want / 4) + 4095) & ~(size_t)4095;
+  hipError_t e = hipHostMalloc((void**)p, n, hipHostMallocCoherent);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc(coherent)");
+  void* d = nullptr;
+  e = hipHostGetDevicePointer(&d, *p, 0);
+  if (e != hipSuccess || d != *p) {
+    hipHostFree(*p);
+    *p = nullptr;
+    return e != hipSuccess ? hip_fail(ctx, e, "hipHostGetDevicePointer")
+                           : set_err(ctx, WGCS_ERR_HIP, "pinned memory is not mapped at its host address");
+  }
+  *cap = n;
+  return WGCS_OK;
+}
+
+uint32_t load_acq(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+
+int launch(wgcs_ring* rg, uint32_t last) {
+  hipSetDevice(rg->ctx->device);
+  const hipError_t e = launch_ring(rg->ctl, rg->nb, last, rg->idle_ticks, rg->stream);
+  if (e != hipSuccess) return hip_fail(rg->ctx, e, "ring_kernel launch");
+  ++rg->launches;
+  return WGCS_OK;
+}
+
+// Post the request record (filled by the caller) and wait for every
+// workgroup's completion.  Caller holds rg->mu.
+int post_and_wait(wgcs_ring* rg) {
+  RingReq* rq = &rg->ctl->req;
+  const uint32_t target = load_acq(&rg->ctl->dn.done) + rg->nb;
+  const uint32_t q = ++rg->seq;
+  if (q == 0xFFFFFFFFu) return set_err(rg->ctx, WGCS_ERR_INVALID_ARG, "ring: request numbers exhausted");
+  __atomic_store_n(&rq->seq, q, __ATOMIC_RELEASE);  // after every field of the record
+  ++rg->requests;
+  // the kernel may have left on its idle deadline: launch it again, telling
+  // it the last request it has seen (it then serves q at once)
+  if (hipStreamQuery(rg->stream) == hipSuccess) {
+    const int rc = launch(rg, q - 1);
+    if (rc) return rc;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spin = 1;; ++spin) {
+    if ((int32_t)(load_acq(&rg->ctl->dn.done) - target) >= 0) return WGCS_OK;
+    if ((spin & 4095) == 0) {
+      // the kernel left (idle deadline) between our query and the post: relaunch
+      const hipError_t st = hipStreamQuery(rg->stream);
+      if (st == hipSuccess) {
+        if ((int32_t)(load_acq(&rg->ctl->dn.done) - target) >= 0) return WGCS_OK;
+        const int rc = launch(rg, q - 1);
+        if (rc) return rc;
+      } else if (st != hipErrorNotReady) {
+        return hip_fail(rg->ctx, st, "ring_kernel");
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+        return set_err(rg->ctx, WGCS_ERR_HIP, "ring: request %u not served within 5 s", q);
+    }
+  }
+}
+
+}  // namespace
+
+namespace wgcs {
+
+// handleVirtioRead's device step through the ring: the job's bytes at vbuf
+// (coherent memory), segments into the ring's staging at i * pitch, int32
+// sizes[kbufs] | count | status after them.  Returns the staging pointers.
+int ring_gso_prepare(wgcs_ring* rg, uint32_t kbufs, size_t region, uint8_t** hs, int32_t** meta) {
+  const size_t mbytes = ((size_t)kbufs * 4 + 16 + 15) & ~(size_t)15;
+  const size_t roff = (mbytes + 255) & ~(size_t)255;
+  const int rc = grow_coherent(rg->ctx, &rg->stage, &rg->stage_cap, roff + region + 16);
+  if (rc) return rc;
+  *meta = (int32_t*)rg->stage;
+  *hs = rg->stage + roff;
+  return WGCS_OK;
+}
+int ring_gso(wgcs_ring* rg, const uint8_t* vbuf, uint32_t vlen, uint32_t jflags, uint32_t kbufs, uint32_t pitch,
+             uint32_t room, uint32_t posflags, size_t region, uint8_t** hs, int32_t** meta) {
+  int rc = ring_gso_prepare(rg, kbufs, region, hs, meta);
+  if (rc) return rc;
+  RingReq* rq = &rg->ctl->req;
+  rq->op = kRingOpVirtioRead;
+  rq->vbuf = (uint64_t)(uintptr_t)vbuf;
+  rq->vlen = vlen;
+  rq->jflags = jflags;
+  rq->kbufs = kbufs;
+  rq->pitch = pitch;
+  rq->room = room;
+  rq->posflags = posflags;
+  rq->out = (uint64_t)(uintptr_t)*hs;
+  rq->meta = (uint64_t)(uintptr_t)*meta;
+  return post_and_wait(rg);
+}
+
+// The request bytes as the kernel may read them: caller memory from
+// wgcs_host_alloc as it is, anything else copied into the ring's staging.
+int ring_input(wgcs_ring* rg, const uint8_t* p, size_t n, const uint8_t** out) {
+  if (n == 0 || host_mapped(rg->ctx, p, n)) {
+    *out = p;
+    return WGCS_OK;
+  }
+  const int rc = grow_coherent(rg->ctx, &rg->in, &rg->in_cap, n + 64);
+  if (rc) return rc;
+  memcpy(rg->in, p, n);
+  *out = rg->in;
+  return WGCS_OK;
+}
+
+std::mutex& ring_mutex(wgcs_ring* rg) { return rg->mu; }
+wgcs_ctx* ring_ctx(wgcs_ring* rg) { return rg->ctx; }
+
+}  // namespace wgcs
+
+extern "C" {
+
+int wgcs_ring_create(wgcs_ctx* ctx, uint32_t idle_us, wgcs_ring** out) {
+  if (!ctx || !out) return WGCS_ERR_INVALID_ARG;
+  *out = nullptr;
+  hipSetDevice(ctx->device);
+  wgcs_ring* rg = new wgcs_ring;
+  rg->ctx = ctx;
+  rg->idle_ticks = (uint64_t)(idle_us ? idle_us : 100000) * 100;  // s_memrealtime: 100 MHz
+  hipError_t e = hipStreamCreateWithFlags(&rg->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete rg;
+    return hip_fail(ctx, e, "hipStreamCreate");
+  }
+  uint8_t* c = nullptr;
+  size_t cc = 0;
+  int rc = grow_coherent(ctx, &c, &cc, sizeof(RingCtl));
+  if (rc) {
+    hipStreamDestroy(rg->stream);
+    delete rg;
+    return rc;
+  }
+  rg->ctl = (RingCtl*)c;
+  memset(rg->ctl, 0, sizeof(RingCtl));
+  *out = rg;
+  return WGCS_OK;
+}
+
+int wgcs_ring_destroy(wgcs_ring* rg) {
+  if (!rg) return WGCS_ERR_INVALID_ARG;
+  {
+    std::lock_guard<std::mutex> g(rg->mu);
+    hipSetDevice(rg->ctx->device);
+    __atomic_store_n(&rg->ctl->req.stop, 1u, __ATOMIC_RELEASE);
+    hipStreamSynchronize(rg->stream);  // every workgroup leaves on the stop word
+    hipStreamDestroy(rg->stream);
+    hipHostFree(rg->ctl);
+    if (rg->in) hipHostFree(rg->in);
+    if (rg->stage) hipHostFree(rg->stage);
+  }
+  delete rg;
+  return WGCS_OK;
+}
+
+int wgcs_ring_info(wgcs_ring* rg, uint64_t* requests, uint64_t* launches, int* running) {
+  if (!rg) return WGCS_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(rg->mu);
+  if (requests) *requests = rg->requests;
+  if (launches) *launches = rg->launches;
+  if (running) *running = hipStreamQuery(rg->stream) == hipErrorNotReady ? 1 : 0;
+  return WGCS_OK;
+}
+
+// checksumValid through the ring: wgcs_checksum_valid_cap's arguments and errors.
+int wgcs_ring_checksum_valid_cap(wgcs_ring* rg, const uint8_t* pkt, size_t len, size_t cap, uint8_t iph_len,
+                                 uint8_t proto, int is_v6, int* valid) {
+  if (!rg || !valid || (!pkt && cap) || cap < len) return WGCS_ERR_INVALID_ARG;
+  wgcs_ctx* ctx = rg->ctx;
+  const size_t need = is_v6 ? 40 : 20;
+  if (cap < need || len < iph_len)
+    return set_err(ctx, WGCS_ERR_OUT_OF_RANGE, "pkt[%u:] or its addresses past the slice", (unsigned)iph_len);
+  if (len >= 0x80000000u) return set_err(ctx, WGCS_ERR_INVALID_ARG, "packet too large");
+  std::lock_guard<std::mutex> g(rg->mu);
+  const uint8_t* p = nullptr;
+  int rc = ring_input(rg, pkt, std::max(len, need), &p);
+  if (rc) return rc;
+  RingReq* rq = &rg->ctl->req;
+  rq->op = kRingOpChecksumValid;
+  rq->pkt = (uint64_t)(uintptr_t)p;
+  rq->len = (uint32_t)len;
+  rq->cs = iph_len;
+  rq->proto = proto;
+  rq->flags = is_v6 ? WGCS_PKT_V6 : 0u;
+  if ((rc = post_and_wait(rg))) return rc;
+  *valid = (int)__atomic_load_n(&rg->ctl->dn.valid, __ATOMIC_ACQUIRE);
+  return WGCS_OK;
+}
+
+int wgcs_ring_checksum_valid(wgcs_ring* rg, const uint8_t* pkt, size_t len, uint8_t iph_len, uint8_t proto,
+                             int is_v6, int* valid) {
+  return wgcs_ring_checksum_valid_cap(rg, pkt, len, len, iph_len, proto, is_v6, valid);
+}
+
+}  // extern "C"

@@ -39,6 +39,18 @@ bool wstager_references(wgcs_wstager* ws, uintptr_t a, uintptr_t b);
 int gso_split_staged(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflags, uint8_t* const* bufs,
                      const size_t* buf_lens, int nbufs, int* sizes, int offset, int* status, int* count);
 
+// The resident per-call ring (ring.cpp): staging for one handleVirtioRead
+// (segments at hs + i * pitch, int32 sizes[kbufs] | count | status at meta),
+// its post-and-wait, the request bytes as the kernel may read them (caller
+// memory from wgcs_host_alloc as it is, else a copy), the ring's lock and
+// context.  Caller of ring_gso* / ring_input holds ring_mutex.
+int ring_gso_prepare(wgcs_ring* rg, uint32_t kbufs, size_t region, uint8_t** hs, int32_t** meta);
+int ring_gso(wgcs_ring* rg, const uint8_t* vbuf, uint32_t vlen, uint32_t jflags, uint32_t kbufs, uint32_t pitch,
+             uint32_t room, uint32_t posflags, size_t region, uint8_t** hs, int32_t** meta);
+int ring_input(wgcs_ring* rg, const uint8_t* p, size_t n, const uint8_t** out);
+std::mutex& ring_mutex(wgcs_ring* rg);
+wgcs_ctx* ring_ctx(wgcs_ring* rg);
+
 }  // namespace wgcs
 
 struct wgcs_ctx {

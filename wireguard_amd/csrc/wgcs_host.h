@@ -42,6 +42,41 @@ struct GsoOutPos {
   uint32_t pitch;
   uint32_t flags;  // kOutPosTails
 };
+// The resident per-call ring (ring.cpp, ring_kernel in gso_kernels.hip): one
+// request record the host fills and then publishes by storing `seq` last, and
+// the device's completion record on a line of its own; both in fine-grained
+// (coherent) pinned host memory.
+enum : uint32_t { kRingOpChecksumValid = 1, kRingOpVirtioRead = 2 };
+struct RingReq {
+  uint32_t seq;   // request number, stored last (release); 0: none yet
+  uint32_t op;    // kRingOp*
+  uint32_t stop;  // 1: the kernel exits
+  uint32_t pad0;
+  // checksumValid(pkt[0:len] (addresses up to cap), iphLen = cs, proto, isV6 = flags & WGCS_PKT_V6)
+  uint64_t pkt;
+  uint32_t len, cs, proto, flags;
+  // handleVirtioRead of one read: [virtio hdr | packet] at vbuf (vlen bytes,
+  // job flags jflags), segment i at out + i * pitch, int32 sizes[kbufs] |
+  // count | status at meta
+  uint64_t vbuf;
+  uint32_t vlen, jflags, kbufs, pitch, room, posflags;
+  uint64_t out;
+  uint64_t meta;
+  uint32_t pad1[10];
+};
+struct RingDone {
+  uint32_t done;    // workgroups that finished a request, cumulative
+  uint32_t valid;   // checksumValid's result of the last request
+  uint32_t exited;  // workgroups that left the kernel, cumulative
+  uint32_t pad[13];
+};
+struct RingCtl {
+  RingReq req;
+  uint32_t pad[16];
+  RingDone dn;
+};
+static_assert(sizeof(RingReq) % 64 == 0 && offsetof(RingCtl, dn) % 64 == 0, "the two records on lines of their own");
+
 // Packed-layout pitch and segment bound of one job ([10-byte virtio header |
 // packet], n bytes) from its virtio header and job flags: every segment
 // gso_rows_kernel can write for it fits in `pitch` (a segment is at most

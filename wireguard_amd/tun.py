@@ -306,6 +306,61 @@ class Device:
         return list(tw)[: ntw.value], order, list(clens), self._err(rc)
 
 
+class Ring:
+    """The resident per-call ring (include/wgcsum.h wgcs_ring_*): the per-call
+    checksumValid / handleVirtioRead without a kernel launch per call -- a
+    resident kernel serves request records posted in coherent pinned memory.
+    Same arguments, results and errors as Device.checksum_valid /
+    Device.handle_virtio_read.  Request bytes in Device.host_alloc memory are
+    read in place (zero-copy); other arrays are copied into the ring's staging."""
+
+    def __init__(self, dev: Device, idle_us: int = 0):
+        self.dev, self.lib = dev, dev.lib
+        h = C.c_void_p()
+        dev._check(self.lib.wgcs_ring_create(dev.h, idle_us, C.byref(h)))
+        self.h = h
+        dev._stagers.add(self)  # destroyed before the context
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.wgcs_ring_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self) -> dict:
+        """requests served, kernel launches made, and whether the kernel is resident now"""
+        r, l, on = C.c_uint64(0), C.c_uint64(0), C.c_int(0)
+        self.dev._check(self.lib.wgcs_ring_info(self.h, C.byref(r), C.byref(l), C.byref(on)))
+        return {"requests": r.value, "launches": l.value, "running": bool(on.value)}
+
+    def checksum_valid(self, pkt, iph_len: int, proto: int, is_v6: bool, n: int | None = None) -> bool:
+        """checksumValid(pkt, iphLen, proto, isV6) -- tun/gro.go:554 (as Device.checksum_valid)."""
+        a = _np_u8(bytes(pkt) if not isinstance(pkt, np.ndarray) else pkt)
+        v = C.c_int(0)
+        ln = len(a) if n is None else n
+        self.dev._check(self.lib.wgcs_ring_checksum_valid_cap(self.h, _ptr(a), ln, len(a), iph_len, proto,
+                                                              int(is_v6), C.byref(v)))
+        return bool(v.value)
+
+    def handle_virtio_read(self, read_buf, bufs: list, sizes: list, offset: int, n_read: int | None = None):
+        """handleVirtioRead(readBuf, bufs, sizes, offset) (int, error) -- tun/tun.go:514
+        (as Device.handle_virtio_read)."""
+        a = _np_u8(read_buf)
+        arr, lens = Device._bufs(bufs)
+        csz = (C.c_int * len(bufs))()
+        n = C.c_int(0)
+        nr = len(a) if n_read is None else n_read
+        rc = self.lib.wgcs_ring_handle_virtio_read_cap(self.h, _ptr(a), nr, len(a), arr, lens, len(bufs), csz, offset,
+                                                       C.byref(n))
+        sizes[: len(bufs)] = list(csz)
+        return n.value, self.dev._err(rc)
+
+
 class Stager:
     """Tun.Read batch staging ring (include/wgcsum.h wgcs_stager_*): many TUN
     reads -> one GSO-split launch with pipelined H2D / kernel / D2H.
