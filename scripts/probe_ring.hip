@@ -30,8 +30,7 @@ struct Done {  // device -> host: per workgroup {seq, result}, each on its own 6
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// loads: 0 = sc0 sc1 buffer loads; 1/2/3 = plain loads (after buffer_inv sc0 /
-// buffer_inv sc1 / nothing at the request's start)
+// loads: 0 = sc0 sc1 buffer loads; otherwise plain loads
 __device__ __forceinline__ uint32_t sum_bytes(const uint8_t* src, uint32_t n, int nb, int loads) {
   uint32_t acc = 0;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), (short)0, (int)n, 0x00020000);
@@ -72,8 +71,8 @@ __global__ __launch_bounds__(256) void ring_probe(Req* rq, Done* dn, uint64_t de
         s_sum = 0;
       }
     }
-    if (threadIdx.x < 64 && loads == 1) asm volatile("buffer_inv sc0\n\ts_waitcnt vmcnt(0)" ::: "memory");
-    if (threadIdx.x < 64 && loads == 2) asm volatile("buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
+    // (a hand-written cache invalidate here, loads 1 / 2 in an earlier
+    // version, left the GPU faulted on the box: removed; loads 1-3 = plain)
     __syncthreads();
     const uint32_t q = s_seq;
     if (q == 0xFFFFFFFFu) break;

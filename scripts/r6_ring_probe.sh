@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-r6_ring_probe3}; mkdir -p $OUT
-for a in "1 0 1" "1 0 2" "1 0 3" "3 0 0" "8 0 0"; do
+for a in "1 0 0" "3 0 0" "8 0 0"; do
   timeout -k 5 60 ./scripts/probe_so/probe_ring $a > $OUT/p.txt 2>&1; rc=$?; grep '"ring"' $OUT/p.txt >> $OUT/all.jsonl; [ $rc -eq 0 ] || { cat $OUT/p.txt; exit $rc; }
 done
 cat $OUT/all.jsonl

@@ -106,6 +106,9 @@ __device__ __forceinline__ uint4 wave_desc(const uint4* __restrict__ pkts, uint3
   return r;
 }
 
+#ifndef WGCS_CS_ACC2
+#define WGCS_CS_ACC2 1  // two accumulator chains per lane (0: one, round 5)
+#endif
 #ifndef WGCS_CS_BLOCK
 #define WGCS_CS_BLOCK 256  // threads per block (A/B builds: 512, 1024)
 #endif
@@ -216,6 +219,19 @@ __global__ __launch_bounds__(WGCS_CS_BLOCK) void checksum_batch_kernel(uint8_t* 
         edge_pending = false;
       }
       acc = (acc >> 16) + (acc & 0xFFFFu);  // keep the u32 partial sum far from overflow (huge packets)
+#if WGCS_CS_ACC2
+      // two independent v_dot2 chains (x,y / z,w), joined once per iteration:
+      // half the serial dependency length of one chain of 4U (round 6)
+      uint32_t acc2 = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc = add_halves(acc, v[u].x);
+        acc2 = add_halves(acc2, v[u].z);
+        acc = add_halves(acc, v[u].y);
+        acc2 = add_halves(acc2, v[u].w);
+      }
+      acc += acc2;  // < 2^17 + 16 U x 2^17: no overflow
+#else
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         acc = add_halves(acc, v[u].x);
@@ -223,6 +239,7 @@ __global__ __launch_bounds__(WGCS_CS_BLOCK) void checksum_batch_kernel(uint8_t* 
         acc = add_halves(acc, v[u].z);
         acc = add_halves(acc, v[u].w);
       }
+#endif
     }
     // all lanes converge here: per-lane fold, group sum, parity, pseudo/initial
     uint32_t s = fold32_16(acc);

@@ -41,7 +41,7 @@ constexpr int kMaxHdrLen = 240;  // header bytes held by the 16 lanes of a row (
 
 enum : int { GSO_NONE = 0, GSO_TCPV4 = 1, GSO_TCPV6 = 4, GSO_UDP_L4 = 5 };
 
-__device__ __forceinline__ uint32_t u8at(const uint8_t* p) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)*p); }
+__device__ __forceinline__ uint32_t u8at(const uint8_t* p) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)ldg8(p)); }
 __device__ __forceinline__ uint32_t be16at(const uint8_t* p) { return (u8at(p) << 8) | u8at(p + 1); }
 
 // The first 256 bytes of a job ([virtio hdr | packet...]) held across the
@@ -54,10 +54,10 @@ struct HdrBytes {
   __device__ __forceinline__ void load(const uint8_t* vb, int n, int lane) {
     base = vb;
     len = n;
-    r0 = lane < n ? vb[lane] : 0u;
-    r1 = lane + 64 < n ? vb[lane + 64] : 0u;
-    r2 = lane + 128 < n ? vb[lane + 128] : 0u;
-    r3 = lane + 192 < n ? vb[lane + 192] : 0u;
+    r0 = lane < n ? ldg8(vb + lane) : 0u;
+    r1 = lane + 64 < n ? ldg8(vb + lane + 64) : 0u;
+    r2 = lane + 128 < n ? ldg8(vb + lane + 128) : 0u;
+    r3 = lane + 192 < n ? ldg8(vb + lane + 192) : 0u;
   }
   __device__ __forceinline__ uint32_t operator()(int k) const {  // k wave-uniform
     if (k >= 256) return u8at(base + k);
@@ -223,7 +223,7 @@ struct GenSeg {
 // readBuf byte x after gsoSplit zeroed its IPv4 checksum and L4 checksum fields
 __device__ __forceinline__ uint32_t rbz(const GenSeg& g, int x) {
   if ((g.v4 && (x == 10 || x == 11)) || x == g.ca || x == g.ca + 1) return 0u;
-  return g.rb[x];
+  return ldg8(g.rb + x);
 }
 
 // byte x of the IP header after the id / length writes (x < csumStart = iphLen)
@@ -283,8 +283,8 @@ __device__ void gso_general_row(const uint8_t* rb, int plen, int type, int ipv, 
   g.ulen = (uint32_t)(uint16_t)(seg_len + (hdr_len - cs));  // :1462-1465
   g.id45 = 0;
   if (g.v4) {  // pkt[4:6] after copy(pkt, readBuf[:iphLen]); bytes past iphLen are what bufs[i] held (:1427)
-    const uint32_t b4 = 4 < cs ? rbz(g, 4) : (uint32_t)dst[4];
-    const uint32_t b5 = 5 < cs ? rbz(g, 5) : (uint32_t)dst[5];
+    const uint32_t b4 = 4 < cs ? rbz(g, 4) : ldg8(dst + 4);
+    const uint32_t b5 = 5 < cs ? rbz(g, 5) : ldg8(dst + 5);
     g.id45 = (b4 << 8) | b5;
     if (i > 0) g.id45 = (g.id45 + 1) & 0xFFFFu;  // quirk: id0 + 1 (:1426-1431)
   }
@@ -354,7 +354,7 @@ __device__ void gso_general_row(const uint8_t* rb, int plen, int type, int ipv, 
     }
     if (g.tcp) {
       for (int t = 0; t < 4; ++t) put(g.s4 + t, (g.seq >> (24 - 8 * t)) & 0xFFu);
-      if (!g.last && g.f13 >= g.pkt_len) dst[g.f13] = (uint8_t)(dst[g.f13] & ~0x09u);
+      if (!g.last && g.f13 >= g.pkt_len) dst[g.f13] = (uint8_t)(ldg8(dst + g.f13) & ~0x09u);
     } else {
       put(g.s4, g.ulen >> 8);
       put(g.s4 + 1, g.ulen & 0xFFu);
@@ -546,7 +546,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t job_rsrc(const uint8_t* vb, ui
 }
 template <bool NT>
 __device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t rs, int off) {
-  const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, NT ? 2 : 0);
+  const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, WGCS_LD_AUX(NT));
   return make_uint4(t[0], t[1], t[2], t[3]);
 }
 // One batch of dword-aligned windows: lane r loads windows k0 + r + 16u at job
@@ -568,7 +568,7 @@ __device__ __forceinline__ void load_windows(__amdgpu_buffer_rsrc_t rs, int aoff
   }
   const int oe = aoff + 16 * (k0 + 16 * U);
   E = __builtin_amdgcn_raw_buffer_load_b32(rs, (r == 15 && oe < hi && oe + 4 > lo) ? oe : kOobOffset, 0,
-                                           NT ? 2 : 0);
+                                           WGCS_LD_AUX(NT));
 }
 
 // Wave-uniform: no lane of the wave has `pred` set (a scalar compare, no exec-mask branch).
@@ -1223,6 +1223,7 @@ __device__ __forceinline__ void gso_rows_body(const uint8_t* arena, const wgcs_g
   }
 }
 
+#ifndef WGCS_RING_TU  // the batch kernels and their launchers: gso_kernels.hip only
 template <int U, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WAVES, 8))) void gso_rows_kernel(const uint8_t* __restrict__ arena,
                                                        const wgcs_gso_job* __restrict__ jobs, uint32_t max_segs,
@@ -1236,6 +1237,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
                        outpos != nullptr, pos, offset, room, sizes, count, status);
 }
 
+#endif  // !WGCS_RING_TU
+#ifdef WGCS_RING_TU  // the ring kernel: ring_kernels.hip only
 // ---------------------------------------------------------------------------
 // The resident per-call ring (round 6).  A launch plus a
 // completion wait costs ~20 us per Go call, more than the Go
@@ -1250,12 +1253,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGCS_GSO_WA
 // loop on the stop word or when no request came for `idle_ticks` of
 // s_memrealtime (100 MHz), so no launch can outlive its use.
 
-__device__ __forceinline__ uint32_t ld_sys32(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
+typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
 
 // checksumValid(pkt, iphLen, proto, isV6) (gro.go:554-612) by one wave: the
 // batch kernel's VALIDATE arithmetic (checksum_kernels.hip) over every chunk
@@ -1297,85 +1295,98 @@ __device__ uint32_t ring_validate(const uint8_t* pkt, int len, int cs, int proto
 
 __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0, uint64_t idle_ticks) {
   __shared__ uint32_t s_q;
-  __shared__ RingReq s_r;
+  __shared__ uint32_t s_w[32];  // the request record's words
   RingReq* const rq = &ctl->req;
   uint32_t last = last0;
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    if (threadIdx.x == 0) {
-      uint32_t q;
+    if (threadIdx.x < 64) {
+      // wave 0 polls the whole 128-B record with ONE system-scope load per
+      // poll (lanes 0-7: 16 B each), so the request's fields arrive with its
+      // number -- one PCIe round trip, not one per field
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(rq, (short)0, (int)sizeof(RingReq),
+                                                                          0x00020000);
+      const int part = threadIdx.x & 7;
+      uint32_t q = 0;
+      u32x4s v;
       for (;;) {
-        q = ld_sys32(&rq->seq);
-        if (ld_sys32(&rq->stop)) {
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * part, 0, 17);  // sc0 sc1
+        q = (uint32_t)__builtin_amdgcn_readlane((int)v[0], 0);
+        const uint32_t stop = (uint32_t)__builtin_amdgcn_readlane((int)v[kRqStop & 3], 0);
+        if (stop) {
           q = 0xFFFFFFFFu;
           break;
         }
-        if (q != last) break;
+        // all eight chunks carry the same new seq: an untorn record
+        const bool same = __builtin_amdgcn_ballot_w64(threadIdx.x < 8 && v[0] != q) == 0;
+        if (q != last && same) break;
         if (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
           q = 0xFFFFFFFFu;
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
       }
-      s_q = q;
-      if (q != 0xFFFFFFFFu) {  // the request's fields, stored by the host before seq
-        s_r.op = ld_sys32(&rq->op);
-        s_r.pkt = ld_sys64(&rq->pkt);
-        s_r.len = ld_sys32(&rq->len);
-        s_r.cs = ld_sys32(&rq->cs);
-        s_r.proto = ld_sys32(&rq->proto);
-        s_r.flags = ld_sys32(&rq->flags);
-        s_r.vbuf = ld_sys64(&rq->vbuf);
-        s_r.vlen = ld_sys32(&rq->vlen);
-        s_r.jflags = ld_sys32(&rq->jflags);
-        s_r.kbufs = ld_sys32(&rq->kbufs);
-        s_r.pitch = ld_sys32(&rq->pitch);
-        s_r.room = ld_sys32(&rq->room);
-        s_r.posflags = ld_sys32(&rq->posflags);
-        s_r.out = ld_sys64(&rq->out);
-        s_r.meta = ld_sys64(&rq->meta);
+      if (threadIdx.x < 8) {
+        s_w[4 * part] = v[0];
+        s_w[4 * part + 1] = v[1];
+        s_w[4 * part + 2] = v[2];
+        s_w[4 * part + 3] = v[3];
       }
+      if (threadIdx.x == 0) s_q = q;
     }
     __syncthreads();
     const uint32_t q = s_q;
     if (q == 0xFFFFFFFFu) break;  // block-uniform: every wave leaves
-    const uint32_t op = (uint32_t)ufl((int)s_r.op);
+    auto w = [&](uint32_t k) { return (uint32_t)ufl((int)s_w[k]); };
+    auto p64 = [&](uint32_t lo, uint32_t hi) { return (uint64_t)w(lo) | ((uint64_t)w(hi) << 32); };
+    const uint32_t op = w(kRqOp);
+    uint32_t valid = 0;
     if (op == kRingOpChecksumValid) {
-      if (blockIdx.x == 0 && threadIdx.x < 64) {
-        const uint32_t v = ring_validate(reinterpret_cast<const uint8_t*>(s_r.pkt), (int)s_r.len, (int)s_r.cs,
-                                         (int)s_r.proto, (s_r.flags & WGCS_PKT_V6) != 0);
-        if (threadIdx.x == 0) __hip_atomic_store(&ctl->dn.valid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
+      if (blockIdx.x == 0 && threadIdx.x < 64)
+        valid = ring_validate(reinterpret_cast<const uint8_t*>(p64(kRqPktLo, kRqPktHi)), (int)w(kRqLen),
+                              (int)w(kRqCs), (int)w(kRqProto), (w(kRqFlags) & WGCS_PKT_V6) != 0);
     } else if (op == kRingOpVirtioRead) {
-      const wgcs_gso_job job = {0, s_r.vlen, s_r.jflags};
-      const GsoOutPos pos = {0, s_r.pitch, s_r.posflags};
-      int32_t* h = reinterpret_cast<int32_t*>(s_r.meta);
-      const uint32_t kb = s_r.kbufs;
-      gso_rows_body<WGCS_GSO_U, false>(reinterpret_cast<const uint8_t*>(s_r.vbuf), job, 0, (int)blockIdx.x,
-                                       (int)gridDim.x, kb, reinterpret_cast<uint8_t*>(s_r.out), 0, true, pos, 0,
-                                       s_r.room, h, h + kb, h + kb + 1);
+      const wgcs_gso_job job = {0, w(kRqVlen), w(kRqJflags)};
+      const GsoOutPos pos = {0, w(kRqPitch), w(kRqPosFlags)};
+      int32_t* h = reinterpret_cast<int32_t*>(p64(kRqMetaLo, kRqMetaHi));
+      const uint32_t kb = w(kRqKbufs);
+      gso_rows_body<WGCS_GSO_U, false>(reinterpret_cast<const uint8_t*>(p64(kRqVbufLo, kRqVbufHi)), job, 0,
+                                       (int)blockIdx.x, (int)gridDim.x, kb,
+                                       reinterpret_cast<uint8_t*>(p64(kRqOutLo, kRqOutHi)), 0, true, pos, 0,
+                                       w(kRqRoom), h, h + kb, h + kb + 1);
     }
-    // completion: every wave's stores done, then one release at system scope
-    // and the count (the fence's own wait is made explicit: MI355X_MICROARCH.md)
+    // completion: every wave's stores done; a request that stored results
+    // releases them at system scope (the fence's own wait made explicit:
+    // MI355X_MICROARCH.md); then {seq, valid} in ONE 8-byte write-through
+    // store on this workgroup's own line, which the host spins on
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(&ctl->dn.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (op == kRingOpVirtioRead) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      const __amdgpu_buffer_rsrc_t ds = __builtin_amdgcn_make_buffer_rsrc(&ctl->dn[blockIdx.x], (short)0, 64,
+                                                                          0x00020000);
+      const u32x2 w = {q, valid};
+      __builtin_amdgcn_raw_buffer_store_b64(w, ds, 0, 0, 17);  // sc0 sc1
     }
     last = q;
     t_last = __builtin_amdgcn_s_memrealtime();
   }
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(&ctl->dn.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(&ctl->dn[blockIdx.x].exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 hipError_t launch_ring(RingCtl* ctl, uint32_t nb, uint32_t last, uint64_t idle_ticks, hipStream_t s) {
-  if (nb == 0 || nb > 64) return hipErrorInvalidValue;
+  if (nb == 0 || nb > kRingMaxBlocks) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ring_kernel, dim3(nb), dim3(256), 0, s, ctl, last, idle_ticks);
   return hipGetLastError();
 }
 
+#endif  // WGCS_RING_TU
+#ifndef WGCS_RING_TU
 // ---------------------------------------------------------------------------
 // Job staged whole in LDS (round 5): one workgroup of NW waves per job.
 //
@@ -2191,4 +2202,5 @@ hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs
   return hipGetLastError();
 }
 
+#endif  // !WGCS_RING_TU
 }  // namespace wgcs

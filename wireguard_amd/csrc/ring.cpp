@@ -82,12 +82,24 @@ int launch(wgcs_ring* rg, uint32_t last) {
 
 // Post the request record (filled by the caller) and wait for every
 // workgroup's completion.  Caller holds rg->mu.
+uint32_t* rq_word(RingReq* rq, uint32_t k) { return &rq->c[k >> 2][k & 3]; }
+void rq_put(RingReq* rq, uint32_t k, uint32_t v) { __atomic_store_n(rq_word(rq, k), v, __ATOMIC_RELAXED); }
+void rq_put64(RingReq* rq, uint32_t lo, uint32_t hi, const void* p) {
+  rq_put(rq, lo, (uint32_t)(uintptr_t)p);
+  rq_put(rq, hi, (uint32_t)((uint64_t)(uintptr_t)p >> 32));
+}
+
+bool served(wgcs_ring* rg, uint32_t q) {
+  for (uint32_t b = 0; b < rg->nb; ++b)
+    if (load_acq(&rg->ctl->dn[b].seq) != q) return false;
+  return true;
+}
+
 int post_and_wait(wgcs_ring* rg) {
   RingReq* rq = &rg->ctl->req;
-  const uint32_t target = load_acq(&rg->ctl->dn.done) + rg->nb;
   const uint32_t q = ++rg->seq;
   if (q == 0xFFFFFFFFu) return set_err(rg->ctx, WGCS_ERR_INVALID_ARG, "ring: request numbers exhausted");
-  __atomic_store_n(&rq->seq, q, __ATOMIC_RELEASE);  // after every field of the record
+  for (int c = 0; c < 8; ++c) __atomic_store_n(&rq->c[c][0], q, __ATOMIC_RELEASE);  // after every field
   ++rg->requests;
   // the kernel may have left on its idle deadline: launch it again, telling
   // it the last request it has seen (it then serves q at once)
@@ -97,12 +109,12 @@ int post_and_wait(wgcs_ring* rg) {
   }
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t spin = 1;; ++spin) {
-    if ((int32_t)(load_acq(&rg->ctl->dn.done) - target) >= 0) return WGCS_OK;
+    if (served(rg, q)) return WGCS_OK;
     if ((spin & 4095) == 0) {
       // the kernel left (idle deadline) between our query and the post: relaunch
       const hipError_t st = hipStreamQuery(rg->stream);
       if (st == hipSuccess) {
-        if ((int32_t)(load_acq(&rg->ctl->dn.done) - target) >= 0) return WGCS_OK;
+        if (served(rg, q)) return WGCS_OK;
         const int rc = launch(rg, q - 1);
         if (rc) return rc;
       } else if (st != hipErrorNotReady) {
@@ -135,16 +147,16 @@ int ring_gso(wgcs_ring* rg, const uint8_t* vbuf, uint32_t vlen, uint32_t jflags,
   int rc = ring_gso_prepare(rg, kbufs, region, hs, meta);
   if (rc) return rc;
   RingReq* rq = &rg->ctl->req;
-  rq->op = kRingOpVirtioRead;
-  rq->vbuf = (uint64_t)(uintptr_t)vbuf;
-  rq->vlen = vlen;
-  rq->jflags = jflags;
-  rq->kbufs = kbufs;
-  rq->pitch = pitch;
-  rq->room = room;
-  rq->posflags = posflags;
-  rq->out = (uint64_t)(uintptr_t)*hs;
-  rq->meta = (uint64_t)(uintptr_t)*meta;
+  rq_put(rq, kRqOp, kRingOpVirtioRead);
+  rq_put64(rq, kRqVbufLo, kRqVbufHi, vbuf);
+  rq_put(rq, kRqVlen, vlen);
+  rq_put(rq, kRqJflags, jflags);
+  rq_put(rq, kRqKbufs, kbufs);
+  rq_put(rq, kRqPitch, pitch);
+  rq_put(rq, kRqRoom, room);
+  rq_put(rq, kRqPosFlags, posflags);
+  rq_put64(rq, kRqOutLo, kRqOutHi, *hs);
+  rq_put64(rq, kRqMetaLo, kRqMetaHi, *meta);
   return post_and_wait(rg);
 }
 
@@ -200,7 +212,7 @@ int wgcs_ring_destroy(wgcs_ring* rg) {
   {
     std::lock_guard<std::mutex> g(rg->mu);
     hipSetDevice(rg->ctx->device);
-    __atomic_store_n(&rg->ctl->req.stop, 1u, __ATOMIC_RELEASE);
+    __atomic_store_n(rq_word(&rg->ctl->req, kRqStop), 1u, __ATOMIC_RELEASE);
     hipStreamSynchronize(rg->stream);  // every workgroup leaves on the stop word
     hipStreamDestroy(rg->stream);
     hipHostFree(rg->ctl);
@@ -234,14 +246,14 @@ int wgcs_ring_checksum_valid_cap(wgcs_ring* rg, const uint8_t* pkt, size_t len, 
   int rc = ring_input(rg, pkt, std::max(len, need), &p);
   if (rc) return rc;
   RingReq* rq = &rg->ctl->req;
-  rq->op = kRingOpChecksumValid;
-  rq->pkt = (uint64_t)(uintptr_t)p;
-  rq->len = (uint32_t)len;
-  rq->cs = iph_len;
-  rq->proto = proto;
-  rq->flags = is_v6 ? WGCS_PKT_V6 : 0u;
+  rq_put(rq, kRqOp, kRingOpChecksumValid);
+  rq_put64(rq, kRqPktLo, kRqPktHi, p);
+  rq_put(rq, kRqLen, (uint32_t)len);
+  rq_put(rq, kRqCs, iph_len);
+  rq_put(rq, kRqProto, proto);
+  rq_put(rq, kRqFlags, is_v6 ? WGCS_PKT_V6 : 0u);
   if ((rc = post_and_wait(rg))) return rc;
-  *valid = (int)__atomic_load_n(&rg->ctl->dn.valid, __ATOMIC_ACQUIRE);
+  *valid = (int)__atomic_load_n(&rg->ctl->dn[0].valid, __ATOMIC_ACQUIRE);
   return WGCS_OK;
 }
 

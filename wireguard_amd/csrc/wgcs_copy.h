@@ -15,7 +15,28 @@ namespace wgcs {
 // All addresses stay pointers derived from kernel arguments (no integer round
 // trips), so the compiler keeps them in the global address space and emits
 // global_load/store (not flat_*, which forces full vmcnt+lgkmcnt waits).
+//
+// WGCS_RING_TU (ring_kernels.hip, the resident per-call ring): the request
+// bytes change between requests at one address while the kernel stays
+// resident, so every load of them is a system-scope one (relaxed atomic: sc0
+// sc1, it misses the CU's L1 and the L2 -- no stale line of an earlier
+// request; no ordering waits).  Elsewhere these are plain loads.
+#ifdef WGCS_RING_TU
+__device__ __forceinline__ uint4 ld16(const uint8_t* a) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(a);
+  const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+__device__ __forceinline__ uint32_t ldg8(const uint8_t* a) {
+  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#define WGCS_LD_AUX(nt) 17  // buffer loads: sc0 sc1
+#else
 __device__ __forceinline__ uint4 ld16(const uint8_t* a) { return *reinterpret_cast<const uint4*>(a); }
+__device__ __forceinline__ uint32_t ldg8(const uint8_t* a) { return *a; }
+#define WGCS_LD_AUX(nt) ((nt) ? 2 : 0)
+#endif
 
 // Funnel: bytes [s, s+16) of the 32-byte concatenation a|b (s wave-uniform).
 __device__ __forceinline__ uint4 funnel(const uint4& a, const uint4& b, int s) {

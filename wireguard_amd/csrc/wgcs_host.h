@@ -47,35 +47,41 @@ struct GsoOutPos {
 // the device's completion record on a line of its own; both in fine-grained
 // (coherent) pinned host memory.
 enum : uint32_t { kRingOpChecksumValid = 1, kRingOpVirtioRead = 2 };
+// The request record: eight 16-byte chunks, each {seq, 3 fields}.  The host
+// stores the fields, then seq into every chunk (x86 stores become visible in
+// order); the GPU reads the record with ONE wave load (lane k: chunk k) and
+// takes it only when all eight seq words agree -- each 16-byte read is a
+// snapshot, so a chunk whose seq is new holds that request's fields, and a
+// record torn between two requests is read again.
 struct RingReq {
-  uint32_t seq;   // request number, stored last (release); 0: none yet
-  uint32_t op;    // kRingOp*
-  uint32_t stop;  // 1: the kernel exits
-  uint32_t pad0;
-  // checksumValid(pkt[0:len] (addresses up to cap), iphLen = cs, proto, isV6 = flags & WGCS_PKT_V6)
-  uint64_t pkt;
-  uint32_t len, cs, proto, flags;
-  // handleVirtioRead of one read: [virtio hdr | packet] at vbuf (vlen bytes,
-  // job flags jflags), segment i at out + i * pitch, int32 sizes[kbufs] |
-  // count | status at meta
-  uint64_t vbuf;
-  uint32_t vlen, jflags, kbufs, pitch, room, posflags;
-  uint64_t out;
-  uint64_t meta;
-  uint32_t pad1[10];
+  uint32_t c[8][4];
 };
+// field positions: chunk, word (word 0 of every chunk is seq)
+enum : uint32_t {
+  kRqOp = 0 * 4 + 1, kRqStop = 0 * 4 + 2, kRqLen = 0 * 4 + 3,           // checksumValid: len
+  kRqCs = 1 * 4 + 1, kRqProto = 1 * 4 + 2, kRqFlags = 1 * 4 + 3,       // iphLen, proto, WGCS_PKT_V6
+  kRqPktLo = 2 * 4 + 1, kRqPktHi = 2 * 4 + 2, kRqVlen = 2 * 4 + 3,     // pkt; virtio read: vlen
+  kRqVbufLo = 3 * 4 + 1, kRqVbufHi = 3 * 4 + 2, kRqJflags = 3 * 4 + 3, // [virtio hdr | packet], job flags
+  kRqKbufs = 4 * 4 + 1, kRqPitch = 4 * 4 + 2, kRqRoom = 4 * 4 + 3,     // slots, segment pitch, bufs[0] room
+  kRqPosFlags = 5 * 4 + 1, kRqOutLo = 5 * 4 + 2, kRqOutHi = 5 * 4 + 3, // kOutPosTails; segment i at out + i pitch
+  kRqMetaLo = 6 * 4 + 1, kRqMetaHi = 6 * 4 + 2,                        // int32 sizes[kbufs] | count | status
+};
+// One per workgroup, each on a 64-B line of its own: {seq, valid} is written
+// by ONE 8-byte write-through store after the request's results.
 struct RingDone {
-  uint32_t done;    // workgroups that finished a request, cumulative
-  uint32_t valid;   // checksumValid's result of the last request
-  uint32_t exited;  // workgroups that left the kernel, cumulative
+  uint32_t seq;     // the request this workgroup finished last
+  uint32_t valid;   // checksumValid's result (workgroup 0)
+  uint32_t exited;  // times this workgroup left the kernel
   uint32_t pad[13];
 };
+enum : uint32_t { kRingMaxBlocks = 8 };
 struct RingCtl {
   RingReq req;
   uint32_t pad[16];
-  RingDone dn;
+  RingDone dn[kRingMaxBlocks];
 };
-static_assert(sizeof(RingReq) % 64 == 0 && offsetof(RingCtl, dn) % 64 == 0, "the two records on lines of their own");
+static_assert(sizeof(RingReq) % 64 == 0 && offsetof(RingCtl, dn) % 64 == 0 && sizeof(RingDone) == 64,
+              "the records on lines of their own");
 
 // Packed-layout pitch and segment bound of one job ([10-byte virtio header |
 // packet], n bytes) from its virtio header and job flags: every segment
