@@ -91,7 +91,15 @@ for fn in ("wgcs_handle_virtio_read",):
         rc = call()
         assert rc == rc_o and cnt.value == n_o and list(sizes)[:n_o] == sz_o[:n_o], (tag, rc, rc_o)
         assert all(np.array_equal(bufs[i], bo[i]) for i in range(nb)), tag
+# the Read buffers as one pinned slab on a fixed stride: segments written in place
+slab = dev.host_alloc(nb * bsz)
+sarr = (u8p * nb)(*[C.cast(slab.ctypes.data + i * bsz, u8p) for i in range(nb)])
+rc = L.wgcs_ring_handle_virtio_read(rh, prb.ctypes.data, n, sarr, lens, nb, sizes, off, C.byref(cnt))
+assert rc == 0 and cnt.value == 45
+assert all(np.array_equal(slab[i * bsz:(i + 1) * bsz], bo[i]) for i in range(nb))
 res["handle_virtio_read"] = {
+    "ring_pinned_direct": med(lambda: L.wgcs_ring_handle_virtio_read(rh, prb.ctypes.data, n, sarr, lens, nb, sizes,
+                                                                     off, C.byref(cnt))),
     "bytes": n, "segments": 45,
     "per_call_launch": med(lambda: L.wgcs_handle_virtio_read(h, rb.ctypes.data, n, arr, lens, nb, sizes, off,
                                                              C.byref(cnt))),
@@ -107,4 +115,5 @@ print(json.dumps(res), flush=True)
 ring.close()
 dev.host_free(ppk)
 dev.host_free(prb)
+dev.host_free(slab)
 dev.close()

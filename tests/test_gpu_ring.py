@@ -151,6 +151,38 @@ def test_ring_handle_virtio_read_pinned_reuse(dev, ring):
         dev.host_free(rb)
 
 
+def test_ring_handle_virtio_read_direct_into_pinned_slab(dev, ring):
+    """Zero-copy both ways: the readBuf and the Read buffers in wgcs_host_alloc
+    memory, the buffers one slab on a fixed stride (a Read-buffer pool), so the
+    kernel writes the segments straight into them; every byte of every buffer
+    (the sentinel fill between and after the packets included) matches the
+    oracle's, for split, GSO_NONE and error reads."""
+    nb, stride, offset = 64, 2048, 16
+    slab = dev.host_alloc(nb * stride)
+    rb = dev.host_alloc(65535 + 64)
+    try:
+        bufs = [slab[i * stride:(i + 1) * stride] for i in range(nb)]
+        cases = [synth.make_super_packet(65535 - 131 * k, 1460 - 3 * k, v6=bool(k & 1), udp=bool(k & 2), seed=300 + k)
+                 for k in range(8)]
+        cases += [vp for vp, nbufs, bufsize, fill, off, h, v6 in list(gso_cases.fuzz_cases(False))[:60]]
+        for k, vp in enumerate(cases):
+            slab[:] = SENT
+            rb_o = np.frombuffer(bytearray(vp), np.uint8).copy()
+            rb[: len(vp)] = rb_o
+            bo = [np.full(stride, SENT, np.uint8) for _ in range(nb)]
+            rc_o, n_o, sz_o = oracle.handle_virtio_read(rb_o, bo, offset)
+            sz_p = [0] * nb
+            n_p, err = ring.handle_virtio_read(rb[: len(vp)], bufs, sz_p, offset)
+            if rc_o == ERR_OUT_OF_RANGE:
+                assert _code(err) == ERR_OUT_OF_RANGE, k
+                continue
+            _assert_same((rc_o, n_o, sz_o, bo, rb_o), (_code(err), n_p, sz_p, [np.array(b) for b in bufs],
+                                                         np.array(rb[: len(vp)])))
+    finally:
+        dev.host_free(rb)
+        dev.host_free(slab)
+
+
 def test_ring_idle_exit_relaunch_and_destroy(dev):
     """The kernel leaves after idle_us without a request (every wave reaches
     the deadline), a later call launches it again and is served, and destroy

@@ -78,16 +78,30 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
           memcpy(hs + (size_t)i * pitch, bufs[i] + offset, std::min<size_t>(pitch, buf_lens[i] - offset));
     }
   };
+  bool direct = false;  // ring: segments straight into the caller's buffers
   if (ring) {
-    // the ring stages the mirror itself: its region is known once it has grown
     uint8_t* rs = nullptr;
     int32_t* rm = nullptr;
-    if ((rc = ring_gso_prepare(ring, (uint32_t)kbufs, region, &rs, &rm))) return rc;
+    // ring-readable caller buffers on a fixed stride (one slab of
+    // wgcs_host_alloc memory, e.g. a pool of Read buffers), each with room for
+    // any segment: the kernel writes segment i at bufs[0] + offset + i * stride
+    // itself, byte for byte what the copy below would leave (no header write
+    // past a packet: !mirror; no slice too short: room >= pitch)
+    const uint32_t nw = std::min<uint32_t>(nseg_bound, (uint32_t)nbufs);
+    if (!mirror && !nobuf && nw > 0) {
+      const ptrdiff_t stride = nw > 1 ? bufs[1] - bufs[0] : (ptrdiff_t)pitch;
+      direct = stride >= (ptrdiff_t)pitch && stride <= 0x7FFFFFFF && (stride & 15) == 0;
+      for (uint32_t i = 0; direct && i < nw; ++i)
+        direct = bufs[i] == bufs[0] + (ptrdiff_t)i * stride && buf_lens[i] >= (size_t)offset + pitch;
+      direct = direct && ring_mapped(ring, bufs[0], (size_t)(nw - 1) * (size_t)stride + (size_t)offset + pitch);
+      if (direct) pitch = (uint32_t)stride;
+    }
+    if ((rc = ring_gso_prepare(ring, (uint32_t)kbufs, direct ? 0 : region, &rs, &rm))) return rc;
     hs = rs;
     h = rm;
-    stage_mirror();
+    if (!direct) stage_mirror();
     if ((rc = ring_gso(ring, vbuf, (uint32_t)vlen, jflags, (uint32_t)kbufs, pitch, (uint32_t)room,
-                       mirror ? kOutPosTails : 0u, region, &rs, &rm)))
+                       mirror ? kOutPosTails : 0u, direct ? bufs[0] + offset : hs, h)))
       return rc;
   } else {
     const size_t meta = ((size_t)kbufs * 4 + 16 + 15) & ~(size_t)15;  // sizes[kbufs] | count | status
@@ -143,7 +157,7 @@ int run_gso_host(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t jflag
       res->count = i;
       return WGCS_OK;
     }
-    memcpy(bufs[i] + offset, hs + (size_t)i * pitch, mirror ? need : (size_t)h[i]);
+    if (!direct) memcpy(bufs[i] + offset, hs + (size_t)i * pitch, mirror ? need : (size_t)h[i]);
   }
   return WGCS_OK;
 }

@@ -622,7 +622,7 @@ __device__ __forceinline__ void consume_batch(const uint4 (&A)[U], uint32_t E, i
       acc = add4(acc, v);
       int ko = 16 * k;
       asm volatile("" : "+v"(ko));
-      *reinterpret_cast<uint4*>(dbase + ko) = v;
+      st128(dbase + ko, v);
     } else if (k < nk) {
       if (x0 >= hdr_len && x0 + 16 <= pkt_len) acc = add4(acc, v);
       else acc = add4_masked(acc, v, byte_bits16(hdr_len - x0, pkt_len - x0), false);
@@ -660,7 +660,7 @@ __device__ __forceinline__ void store16_row(const RowOut& o, uint8_t* dbase, int
     const u32x4v vv = {v.x, v.y, v.z, v.w};
     __builtin_amdgcn_raw_buffer_store_b128(vv, o.rs, o.dro + ko, 0, WGCS_GSO_WT_AUX);
   } else {
-    *reinterpret_cast<uint4*>(dbase + ko) = v;
+    st128(dbase + ko, v);
   }
 }
 // store_chunk with its full-chunk case through store16_row.
@@ -1309,23 +1309,35 @@ __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0,
       const int part = threadIdx.x & 7;
       uint32_t q = 0;
       u32x4s v;
-      for (;;) {
-        v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * part, 0, 17);  // sc0 sc1
-        q = (uint32_t)__builtin_amdgcn_readlane((int)v[0], 0);
-        const uint32_t stop = (uint32_t)__builtin_amdgcn_readlane((int)v[kRqStop & 3], 0);
-        if (stop) {
-          q = 0xFFFFFFFFu;
-          break;
-        }
+      // 0: keep polling; 1: a new untorn record; 2: stop / idle deadline
+      auto check = [&](const u32x4s& x) -> int {
+        q = (uint32_t)__builtin_amdgcn_readlane((int)x[0], 0);
+        if (__builtin_amdgcn_readlane((int)x[kRqStop & 3], 0) != 0) return 2;
         // all eight chunks carry the same new seq: an untorn record
-        const bool same = __builtin_amdgcn_ballot_w64(threadIdx.x < 8 && v[0] != q) == 0;
-        if (q != last && same) break;
-        if (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
-          q = 0xFFFFFFFFu;
+        const bool same = __builtin_amdgcn_ballot_w64(threadIdx.x < 8 && x[0] != q) == 0;
+        if (q != last && same) return 1;
+        if (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) return 2;
+        return 0;
+      };
+      // two polls in flight, issued half a round trip apart: a posted request
+      // is seen ~RTT/4 sooner on average than with one poll at a time
+      u32x4s va = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * part, 0, 17), vb;  // sc0 sc1
+      int st;
+      for (;;) {
+        __builtin_amdgcn_s_sleep(1);
+        vb = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * part, 0, 17);
+        if ((st = check(va)) != 0) {
+          v = va;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
+        va = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * part, 0, 17);
+        if ((st = check(vb)) != 0) {
+          v = vb;
+          break;
+        }
       }
+      if (st == 2) q = 0xFFFFFFFFu;
       if (threadIdx.x < 8) {
         s_w[4 * part] = v[0];
         s_w[4 * part + 1] = v[1];
@@ -1339,21 +1351,23 @@ __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0,
     if (q == 0xFFFFFFFFu) break;  // block-uniform: every wave leaves
     auto w = [&](uint32_t k) { return (uint32_t)ufl((int)s_w[k]); };
     auto p64 = [&](uint32_t lo, uint32_t hi) { return (uint64_t)w(lo) | ((uint64_t)w(hi) << 32); };
+    // request pointers as global-address-space ones: the inlined body then
+    // emits global_load / global_store, not flat (which also waits on lgkmcnt)
+    typedef __attribute__((address_space(1))) uint8_t g8;
+    auto gptr = [&](uint32_t lo, uint32_t hi) { return (uint8_t*)(g8*)(uintptr_t)p64(lo, hi); };
     const uint32_t op = w(kRqOp);
     uint32_t valid = 0;
     if (op == kRingOpChecksumValid) {
       if (blockIdx.x == 0 && threadIdx.x < 64)
-        valid = ring_validate(reinterpret_cast<const uint8_t*>(p64(kRqPktLo, kRqPktHi)), (int)w(kRqLen),
+        valid = ring_validate(gptr(kRqPktLo, kRqPktHi), (int)w(kRqLen),
                               (int)w(kRqCs), (int)w(kRqProto), (w(kRqFlags) & WGCS_PKT_V6) != 0);
     } else if (op == kRingOpVirtioRead) {
       const wgcs_gso_job job = {0, w(kRqVlen), w(kRqJflags)};
       const GsoOutPos pos = {0, w(kRqPitch), w(kRqPosFlags)};
-      int32_t* h = reinterpret_cast<int32_t*>(p64(kRqMetaLo, kRqMetaHi));
+      int32_t* h = (int32_t*)(__attribute__((address_space(1))) int32_t*)(uintptr_t)p64(kRqMetaLo, kRqMetaHi);
       const uint32_t kb = w(kRqKbufs);
-      gso_rows_body<WGCS_GSO_U, false>(reinterpret_cast<const uint8_t*>(p64(kRqVbufLo, kRqVbufHi)), job, 0,
-                                       (int)blockIdx.x, (int)gridDim.x, kb,
-                                       reinterpret_cast<uint8_t*>(p64(kRqOutLo, kRqOutHi)), 0, true, pos, 0,
-                                       w(kRqRoom), h, h + kb, h + kb + 1);
+      gso_rows_body<WGCS_GSO_U, false>(gptr(kRqVbufLo, kRqVbufHi), job, 0, (int)blockIdx.x, (int)gridDim.x, kb,
+                                       gptr(kRqOutLo, kRqOutHi), 0, true, pos, 0, w(kRqRoom), h, h + kb, h + kb + 1);
     }
     // completion: every wave's stores done; a request that stored results
     // releases them at system scope (the fence's own wait made explicit:
@@ -1362,10 +1376,12 @@ __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
+#ifndef WGCS_RING_NOFENCE  // A/B builds: timing without the system-scope release (not exact output)
       if (op == kRingOpVirtioRead) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+#endif
       typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
       const __amdgpu_buffer_rsrc_t ds = __builtin_amdgcn_make_buffer_rsrc(&ctl->dn[blockIdx.x], (short)0, 64,
                                                                           0x00020000);

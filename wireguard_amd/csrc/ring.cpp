@@ -80,8 +80,7 @@ int launch(wgcs_ring* rg, uint32_t last) {
   return WGCS_OK;
 }
 
-// Post the request record (filled by the caller) and wait for every
-// workgroup's completion.  Caller holds rg->mu.
+// The request record's words (wgcs_host.h RingReq).
 uint32_t* rq_word(RingReq* rq, uint32_t k) { return &rq->c[k >> 2][k & 3]; }
 void rq_put(RingReq* rq, uint32_t k, uint32_t v) { __atomic_store_n(rq_word(rq, k), v, __ATOMIC_RELAXED); }
 void rq_put64(RingReq* rq, uint32_t lo, uint32_t hi, const void* p) {
@@ -89,13 +88,20 @@ void rq_put64(RingReq* rq, uint32_t lo, uint32_t hi, const void* p) {
   rq_put(rq, hi, (uint32_t)((uint64_t)(uintptr_t)p >> 32));
 }
 
-bool served(wgcs_ring* rg, uint32_t q) {
-  for (uint32_t b = 0; b < rg->nb; ++b)
+// workgroups [0, nb) have finished request q
+bool served(wgcs_ring* rg, uint32_t q, uint32_t nb) {
+  for (uint32_t b = 0; b < nb; ++b)
     if (load_acq(&rg->ctl->dn[b].seq) != q) return false;
   return true;
 }
 
-int post_and_wait(wgcs_ring* rg) {
+// Post the request record (filled by the caller) and wait for the
+// completion of the workgroups that work on it: every one for a
+// handleVirtioRead, workgroup 0 alone for a checksumValid (the others only
+// note its number; a later record they read torn is read again).  Caller
+// holds rg->mu.
+int post_and_wait(wgcs_ring* rg, uint32_t need = 0) {
+  if (need == 0 || need > rg->nb) need = rg->nb;
   RingReq* rq = &rg->ctl->req;
   const uint32_t q = ++rg->seq;
   if (q == 0xFFFFFFFFu) return set_err(rg->ctx, WGCS_ERR_INVALID_ARG, "ring: request numbers exhausted");
@@ -109,12 +115,12 @@ int post_and_wait(wgcs_ring* rg) {
   }
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t spin = 1;; ++spin) {
-    if (served(rg, q)) return WGCS_OK;
+    if (served(rg, q, need)) return WGCS_OK;
     if ((spin & 4095) == 0) {
       // the kernel left (idle deadline) between our query and the post: relaunch
       const hipError_t st = hipStreamQuery(rg->stream);
       if (st == hipSuccess) {
-        if (served(rg, q)) return WGCS_OK;
+        if (served(rg, q, need)) return WGCS_OK;
         const int rc = launch(rg, q - 1);
         if (rc) return rc;
       } else if (st != hipErrorNotReady) {
@@ -142,10 +148,11 @@ int ring_gso_prepare(wgcs_ring* rg, uint32_t kbufs, size_t region, uint8_t** hs,
   *hs = rg->stage + roff;
   return WGCS_OK;
 }
+// (out, meta from ring_gso_prepare; out may instead be the caller's own
+// buffers -- bufs[0] + offset with segment i at + i * pitch -- when they are
+// ring-readable memory on a fixed stride: gso_api.cpp)
 int ring_gso(wgcs_ring* rg, const uint8_t* vbuf, uint32_t vlen, uint32_t jflags, uint32_t kbufs, uint32_t pitch,
-             uint32_t room, uint32_t posflags, size_t region, uint8_t** hs, int32_t** meta) {
-  int rc = ring_gso_prepare(rg, kbufs, region, hs, meta);
-  if (rc) return rc;
+             uint32_t room, uint32_t posflags, uint8_t* out, int32_t* meta) {
   RingReq* rq = &rg->ctl->req;
   rq_put(rq, kRqOp, kRingOpVirtioRead);
   rq_put64(rq, kRqVbufLo, kRqVbufHi, vbuf);
@@ -155,8 +162,8 @@ int ring_gso(wgcs_ring* rg, const uint8_t* vbuf, uint32_t vlen, uint32_t jflags,
   rq_put(rq, kRqPitch, pitch);
   rq_put(rq, kRqRoom, room);
   rq_put(rq, kRqPosFlags, posflags);
-  rq_put64(rq, kRqOutLo, kRqOutHi, *hs);
-  rq_put64(rq, kRqMetaLo, kRqMetaHi, *meta);
+  rq_put64(rq, kRqOutLo, kRqOutHi, out);
+  rq_put64(rq, kRqMetaLo, kRqMetaHi, meta);
   return post_and_wait(rg);
 }
 
@@ -174,6 +181,7 @@ int ring_input(wgcs_ring* rg, const uint8_t* p, size_t n, const uint8_t** out) {
   return WGCS_OK;
 }
 
+bool ring_mapped(wgcs_ring* rg, const void* p, size_t n) { return host_mapped(rg->ctx, p, n); }
 std::mutex& ring_mutex(wgcs_ring* rg) { return rg->mu; }
 wgcs_ctx* ring_ctx(wgcs_ring* rg) { return rg->ctx; }
 
@@ -252,7 +260,7 @@ int wgcs_ring_checksum_valid_cap(wgcs_ring* rg, const uint8_t* pkt, size_t len, 
   rq_put(rq, kRqCs, iph_len);
   rq_put(rq, kRqProto, proto);
   rq_put(rq, kRqFlags, is_v6 ? WGCS_PKT_V6 : 0u);
-  if ((rc = post_and_wait(rg))) return rc;
+  if ((rc = post_and_wait(rg, 1))) return rc;
   *valid = (int)__atomic_load_n(&rg->ctl->dn[0].valid, __ATOMIC_ACQUIRE);
   return WGCS_OK;
 }

@@ -37,6 +37,17 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* a) { return *reinterpret_ca
 __device__ __forceinline__ uint32_t ldg8(const uint8_t* a) { return *a; }
 #define WGCS_LD_AUX(nt) ((nt) ? 2 : 0)
 #endif
+// Stores of results: plain everywhere.  (Round 6 measured system-scope
+// write-through stores for the ring's results into host memory: 0.5 ms per
+// 64-KiB read instead of 13 us; the ring releases its plain stores once at
+// the end of a request instead.)
+__device__ __forceinline__ void st128(uint8_t* d, const uint4& v) { *reinterpret_cast<uint4*>(d) = v; }
+__device__ __forceinline__ void st64(uint8_t* d, uint32_t a, uint32_t b) {
+  *reinterpret_cast<uint2*>(d) = make_uint2(a, b);
+}
+__device__ __forceinline__ void st32(uint8_t* d, uint32_t a) { *reinterpret_cast<uint32_t*>(d) = a; }
+__device__ __forceinline__ void st16(uint8_t* d, uint16_t a) { *reinterpret_cast<uint16_t*>(d) = a; }
+__device__ __forceinline__ void st8(uint8_t* d, uint8_t a) { *d = a; }
 
 // Funnel: bytes [s, s+16) of the 32-byte concatenation a|b (s wave-uniform).
 __device__ __forceinline__ uint4 funnel(const uint4& a, const uint4& b, int s) {
@@ -111,50 +122,50 @@ __device__ __forceinline__ void store_lo(uint8_t* d, const uint4& v, int hi) {  
   int p = 0;
   uint32_t a = v.x, b = v.y;  // the dwords at p and p + 4
   if (hi & 8) {
-    *reinterpret_cast<uint2*>(d) = make_uint2(v.x, v.y);
+    st64(d, v.x, v.y);
     p = 8;
     a = v.z;
     b = v.w;
   }
   if (hi & 4) {
-    *reinterpret_cast<uint32_t*>(d + p) = a;
+    st32(d + p, a);
     p += 4;
     a = b;
   }
   if (hi & 2) {
-    *reinterpret_cast<uint16_t*>(d + p) = (uint16_t)a;
+    st16(d + p, (uint16_t)a);
     p += 2;
     a >>= 16;
   }
-  if (hi & 1) d[p] = (uint8_t)a;
+  if (hi & 1) st8(d + p, (uint8_t)a);
 }
 __device__ __forceinline__ void store_hi(uint8_t* d, const uint4& v, int lo) {  // bytes [lo, 16), 0 < lo < 16
   const int n = 16 - lo;
   int e = 16;                 // end of the bytes still to store
   uint32_t a = v.w, b = v.z;  // the dwords ending at e and at e - 4
   if (n & 8) {
-    *reinterpret_cast<uint2*>(d + 8) = make_uint2(v.z, v.w);
+    st64(d + 8, v.z, v.w);
     e = 8;
     a = v.y;
     b = v.x;
   }
   if (n & 4) {
-    *reinterpret_cast<uint32_t*>(d + e - 4) = a;
+    st32(d + e - 4, a);
     e -= 4;
     a = b;
   }
   if (n & 2) {
-    *reinterpret_cast<uint16_t*>(d + e - 2) = (uint16_t)(a >> 16);
+    st16(d + e - 2, (uint16_t)(a >> 16));
     e -= 2;
     a <<= 16;
   }
-  if (n & 1) d[e - 1] = (uint8_t)(a >> 24);
+  if (n & 1) st8(d + e - 1, (uint8_t)(a >> 24));
 }
 
 __device__ __forceinline__ void store_chunk(uint8_t* dchunk, const uint4& v, int x0, int pkt_len) {
   const int lo = -x0, hi = pkt_len - x0;  // the chunk's bytes [lo, hi) are stored
   if (lo <= 0 && hi >= 16) {
-    *reinterpret_cast<uint4*>(dchunk) = v;
+    st128(dchunk, v);
     return;
   }
   if (lo <= 0) {
@@ -170,16 +181,17 @@ __device__ __forceinline__ void store_chunk(uint8_t* dchunk, const uint4& v, int
   if (p >= hi) return;
   auto b8 = [&](int q) { return (uint8_t)(dword_at(v, q >> 2) >> (8 * (q & 3))); };
   auto b16 = [&](int q) { return (uint16_t)(dword_at(v, q >> 2) >> (8 * (q & 2))); };  // q even
-  if ((p & 1) && p < hi) { dchunk[p] = b8(p); p += 1; }
-  if ((p & 2) && p + 2 <= hi) { *reinterpret_cast<uint16_t*>(dchunk + p) = b16(p); p += 2; }
-  if ((p & 4) && p + 4 <= hi) { *reinterpret_cast<uint32_t*>(dchunk + p) = dword_at(v, p >> 2); p += 4; }
+  if ((p & 1) && p < hi) { st8(dchunk + p, b8(p)); p += 1; }
+  if ((p & 2) && p + 2 <= hi) { st16(dchunk + p, b16(p)); p += 2; }
+  if ((p & 4) && p + 4 <= hi) { st32(dchunk + p, dword_at(v, p >> 2)); p += 4; }
   if (p + 8 <= hi) {  // p is 0 or 8 here
-    *reinterpret_cast<uint2*>(dchunk + p) = p ? make_uint2(v.z, v.w) : make_uint2(v.x, v.y);
+    if (p) st64(dchunk + p, v.z, v.w);
+    else st64(dchunk + p, v.x, v.y);
     p += 8;
   }
-  if (p + 4 <= hi) { *reinterpret_cast<uint32_t*>(dchunk + p) = dword_at(v, p >> 2); p += 4; }
-  if (p + 2 <= hi) { *reinterpret_cast<uint16_t*>(dchunk + p) = b16(p); p += 2; }
-  if (p < hi) dchunk[p] = b8(p);
+  if (p + 4 <= hi) { st32(dchunk + p, dword_at(v, p >> 2)); p += 4; }
+  if (p + 2 <= hi) { st16(dchunk + p, b16(p)); p += 2; }
+  if (p < hi) st8(dchunk + p, b8(p));
 }
 
 template <bool SUM>

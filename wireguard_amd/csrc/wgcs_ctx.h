@@ -46,7 +46,9 @@ int gso_split_staged(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t j
 // context.  Caller of ring_gso* / ring_input holds ring_mutex.
 int ring_gso_prepare(wgcs_ring* rg, uint32_t kbufs, size_t region, uint8_t** hs, int32_t** meta);
 int ring_gso(wgcs_ring* rg, const uint8_t* vbuf, uint32_t vlen, uint32_t jflags, uint32_t kbufs, uint32_t pitch,
-             uint32_t room, uint32_t posflags, size_t region, uint8_t** hs, int32_t** meta);
+             uint32_t room, uint32_t posflags, uint8_t* out, int32_t* meta);
+// [p, p + n) lies in wgcs_host_alloc memory the ring reads and writes in place
+bool ring_mapped(wgcs_ring* rg, const void* p, size_t n);
 int ring_input(wgcs_ring* rg, const uint8_t* p, size_t n, const uint8_t** out);
 std::mutex& ring_mutex(wgcs_ring* rg);
 wgcs_ctx* ring_ctx(wgcs_ring* rg);
