@@ -39,5 +39,6 @@ want cfg5 && cfg cfg5 --config cfg5 --steps 10 --warmup 2
 want cfg4 && cfg cfg4 --config cfg4 --steps 30 --warmup 3
 want gro4x32 && cfg gro4x32 --config gro_device --gro-shape 4x32 --steps 10 --warmup 2
 want groshuf && cfg groshuf --config gro_device --gro-shape shuffled --steps 10 --warmup 2
+want udpsplit && cfg udpsplit --config udp_split --steps 10 --warmup 2
 for d in $OUT/*_sized; do echo "== $(basename $d)"; python3 scripts/pmc_sized.py $d | cut -c1-400; done
 echo "== done"

@@ -85,8 +85,10 @@ def _split_batch_ref(msgs_list, first):
     return outs
 
 
-@pytest.mark.parametrize("seed", range(3))
-def test_split_messages_batch(dev, seed):
+@pytest.mark.parametrize("seed,in_stride", [(0, 65536), (1, 65536), (2, 65536), (3, 65541), (4, 65664 + 56)])
+def test_split_messages_batch(dev, seed, in_stride):
+    """Landing slots on 128-B lines and off them (odd strides): the rows that
+    share a source line through LDS see every phase of it."""
     import torch
 
     rng = np.random.default_rng(7000 + seed)
@@ -94,7 +96,6 @@ def test_split_messages_batch(dev, seed):
     first = 126
     cases = [split_case(rng, n_msgs=n_msgs, first=first, buf_len=buf_len)[0] for _ in range(B)]
     ns = n_msgs - first
-    in_stride = 65536
     h_in = np.zeros((B * ns, in_stride), dtype=np.uint8)
     n_in = np.zeros(B * n_msgs, dtype=np.int32)
     gso = np.zeros(B * n_msgs, dtype=np.int32)

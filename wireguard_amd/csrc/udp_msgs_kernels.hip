@@ -67,6 +67,14 @@ __device__ __forceinline__ uint4 ld16_nt(const uint8_t* p) {
 #ifndef WGCS_UDP_NTS
 #define WGCS_UDP_NTS 0
 #endif
+#ifndef WGCS_UDP_SPLIT_OWN
+#define WGCS_UDP_SPLIT_OWN 1  // splitMessages: each 128-B source line loaded by one row, shared through LDS (0: A/B builds)
+#endif
+// A row's LDS image: 16 lanes x 16 B x kOwnU windows.  A packet of g bytes
+// needs at most g + 15 (its first window's phase) + 127 (its last line) of it.
+constexpr int kOwnU = 7;
+constexpr int kOwnImg = 16 * 16 * kOwnU;
+constexpr int kOwnMaxG = kOwnImg - 15 - 127;
 __device__ __forceinline__ void put_chunk(uint8_t* dchunk, const uint4& v, int x0, int len) {
   if (WGCS_UDP_NTS && x0 >= 0 && x0 + 16 <= len) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -163,6 +171,7 @@ __global__ __launch_bounds__(256) void udp_split_kernel(const uint8_t* __restric
   // ---- the split loop (scalar state), recording this row's packet
   int base = 0, st = 0;
   int my_i = -1, my_start = 0, my_len = 0;
+  int my_j = 0, my_ncopy = 0, my_g = 0, my_N = 0;  // packet index, packets landed, gsoSize, N of its message
   bool my_zeroed = false;
   for (int t = 0; t < ns; ++t) {
     const int i = (int)first + t;
@@ -183,6 +192,10 @@ __global__ __launch_bounds__(256) void udp_split_kernel(const uint8_t* __restric
       my_start = j * g;  // start of packet j; end_0 = gsoSize (may pass N), end_j = min((j+1)g, N)
       const int end = g == 0 ? N : (j == 0 ? g : min((j + 1) * g, N));
       my_len = end - my_start;
+      my_j = j;
+      my_ncopy = ncopy;
+      my_g = g;
+      my_N = N;
     }
     base += ncopy;
     if (ncopy < num) { st = WGCS_ERR_SPLIT_OVERFLOW; break; }
@@ -192,21 +205,76 @@ __global__ __launch_bounds__(256) void udp_split_kernel(const uint8_t* __restric
     count[b] = base;
     status[b] = st;
   }
-  if (k >= (int)n_msgs) return;
   const uint64_t sk = slot0 + (uint64_t)k;
-  if (k >= base) {
-    if (r == 0) {
-      n_out[sk] = my_zeroed ? 0 : n_in[sk];
-      src_out[sk] = -1;
-    }
-    return;
-  }
-  if (r == 0) {
-    n_out[sk] = my_len;  // copy() length: the source range never exceeds buf_len here
-    src_out[sk] = my_i;
+  const bool active = k < (int)n_msgs && k < base;
+  if (k < (int)n_msgs && r == 0) {
+    n_out[sk] = active ? my_len : my_zeroed ? 0 : n_in[sk];  // copy() length: within buf_len here
+    src_out[sk] = active ? my_i : -1;
   }
   const uint64_t src_slot = (uint64_t)b * (uint64_t)ns + (uint64_t)(my_i - (int)first);  // landing slots only
-  row_copy_dst_aligned<U>(in + src_slot * in_stride + my_start, my_len, out + sk * out_stride, r);
+  const uint8_t* msg = in + src_slot * in_stride;  // the source message (valid when active)
+  uint8_t* dst = out + sk * out_stride;
+  if constexpr (!WGCS_UDP_SPLIT_OWN) {
+    if (active) row_copy_dst_aligned<U>(msg + my_start, my_len, dst, r);
+    return;
+  }
+  // ---- each 128-B source line loaded by ONE row.  Packets j - 1 and j of a
+  // message (rows k - 1 and k of this block) share the line holding byte j*g;
+  // it belongs to row k - 1, which loads up to the end of that line and puts
+  // the windows from floor16(j*g) on in row k's image too.  Row k loads from
+  // the next line boundary on.  Block edges and packets outside
+  // [128, kOwnMaxG] bytes keep the direct row copy (no neighbour shares).
+  __shared__ __attribute__((aligned(16))) uint8_t s_img[16 * kOwnImg];
+  const int row = wv * 4 + (lane >> 4);
+  const bool own = active && my_g >= 128 && my_g <= kOwnMaxG;
+  // offsets from the 128-B line that holds the message's first byte
+  const int o = (int)((uintptr_t)msg & 127u);
+  const uint8_t* line0 = msg - o;
+  const int s = my_start + o, e = my_start + my_len + o, a0 = s & ~15;
+  if (own) {
+    const bool prev = row > 0 && my_j >= 1;               // row k - 1 holds packet j - 1 of this message
+    const bool next = row < 15 && my_j + 1 < my_ncopy;     // row k + 1 holds packet j + 1
+    const int lo = prev ? (s + 127) & ~127 : a0;
+    // next: up to the end of the shared line, within packet j + 1's bytes
+    const int hi = next ? min((e + 127) & ~127, min((my_j + 2) * my_g, my_N) + o) : e;
+    const int e16 = e & ~15;
+    const uint8_t* lim = line0 + hi;
+    uint8_t* img = s_img + row * kOwnImg;
+    uint4 A[kOwnU];
+#pragma unroll
+    for (int u = 0; u < kOwnU; ++u) {
+      const int x = lo + 16 * (r + 16 * u);
+      A[u] = x < hi ? ld_window<WGCS_UDP_SPLIT_NT != 0>(line0 + x, lim) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kOwnU; ++u) {
+      const int x = lo + 16 * (r + 16 * u);
+      if (x < hi) {
+        *reinterpret_cast<uint4*>(img + (x - a0)) = A[u];
+        if (next && x >= e16) *reinterpret_cast<uint4*>(img + kOwnImg + (x - e16)) = A[u];
+      }
+    }
+  }
+  __syncthreads();
+  if (own) {
+    // chunk c = bytes [s + 16c, s + 16c + 16): five dwords of the image from
+    // floor4(s - a0) + 16c, funnelled by s & 3
+    const uint8_t* img = s_img + row * kOwnImg + ((s - a0) & ~3);
+    const int sb = s & 3, nk = (my_len + 15) >> 4;
+#pragma unroll
+    for (int u = 0; u < kOwnU; ++u) {
+      const int c = r + 16 * u;
+      if (c < nk) {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(img + 16 * c, 4));
+        const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+        const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sb), __builtin_amdgcn_alignbyte(d2, d1, sb),
+                                   __builtin_amdgcn_alignbyte(d3, d2, sb), __builtin_amdgcn_alignbyte(d4, d3, sb));
+        put_chunk(dst + 16 * c, v, 16 * c, my_len);
+      }
+    }
+  } else if (active) {
+    row_copy_dst_aligned<U>(msg + my_start, my_len, dst, r);
+  }
 }
 
 // ---------------------------------------------------------------------------
