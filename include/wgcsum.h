@@ -222,6 +222,11 @@ int wgcs_gso_split_batch(wgcs_ctx *ctx, const uint8_t *d_arena, const wgcs_gso_j
                          uint32_t n_jobs, uint8_t *d_out, uint32_t out_stride, uint32_t offset,
                          uint32_t max_segs, int32_t *d_sizes, int32_t *d_count,
                          int32_t *d_status, void *stream);
+/* the shape wgcs_gso_split_batch was compiled to (not a reference interface:
+ * benches and profiles name the kernel from it): lds_waves waves per
+ * workgroup, parts workgroups per read, u chunks per lane in flight; rows = 1
+ * when WGCS_GSO_KERNEL=rows selects the round-4 gso_rows_kernel grid. */
+int wgcs_gso_kernel_shape(int *lds_waves, int *parts, int *u, int *rows);
 
 /* ---- reference-shaped entry points on host buffers (Go-call granularity) ----
  * These stage through the context's pinned ring, run the HIP kernels and copy

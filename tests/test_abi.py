@@ -99,6 +99,16 @@ def test_version_and_errors():
     assert L.wgcs_strerror(-9999) == b"unknown status"
 
 
+def test_gso_kernel_shape_reports_compiled_grid():
+    """gso_bench names the kernel (and its traffic record) from the library's
+    compiled shape, not from constants of its own."""
+    L = wireguard_amd.load()
+    nw, parts, u, rows = (C.c_int(-1) for _ in range(4))
+    assert L.wgcs_gso_kernel_shape(C.byref(nw), C.byref(parts), C.byref(u), C.byref(rows)) == 0
+    assert nw.value in (1, 2, 4, 8, 16) and 1 <= parts.value <= 8 and u.value > 0 and rows.value in (0, 1)
+    assert L.wgcs_gso_kernel_shape(None, None, None, None) == 0
+
+
 def test_no_device_fails_loudly():
     """In this container there is no GPU: the product must refuse, not fall back."""
     L = wireguard_amd.load()

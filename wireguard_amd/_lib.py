@@ -92,6 +92,7 @@ def load() -> C.CDLL:
         "wgcs_checksum_batch": ([vp, i32, C.c_uint, vp, vp, vp, u32, vp, vp], i32),
         "wgcs_checksum_batches": ([vp, i32, C.c_uint, vp, u32, vp, u32, vp, vp], i32),
         "wgcs_gso_split_batch": ([vp, vp, vp, u32, vp, u32, u32, u32, vp, vp, vp, vp], i32),
+        "wgcs_gso_kernel_shape": ([vp, vp, vp, vp], i32),
         "wgcs_handle_gro_batch": ([vp, vp, vp, vp, u32, vp, vp, vp, vp], i32),
         "wgcs_checksum": ([vp, vp, sz, u64, C.POINTER(C.c_uint16)], i32),
         "wgcs_checksum_valid": ([vp, vp, sz, C.c_uint8, C.c_uint8, i32, C.POINTER(i32)], i32),

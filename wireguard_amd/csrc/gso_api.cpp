@@ -208,6 +208,11 @@ int gso_split_staged(wgcs_ctx* ctx, const uint8_t* vbuf, size_t vlen, uint32_t j
 
 extern "C" {
 
+int wgcs_gso_kernel_shape(int* lds_waves, int* parts, int* u, int* rows) {
+  wgcs::gso_kernel_shape(lds_waves, parts, u, rows);
+  return WGCS_OK;
+}
+
 int wgcs_gso_split_batch(wgcs_ctx* ctx, const uint8_t* d_arena, const wgcs_gso_job* d_jobs, uint32_t n_jobs,
                          uint8_t* d_out, uint32_t out_stride, uint32_t offset, uint32_t max_segs, int32_t* d_sizes,
                          int32_t* d_count, int32_t* d_status, void* stream) {

@@ -2183,17 +2183,29 @@ __global__ __launch_bounds__(NW * 64) WGCS_GSO_LDS_ATTR void gso_lds_kernel(cons
   }
 }
 
+// WGCS_GSO_KERNEL=rows selects the round-4 grid (A/B builds and probes)
+static int gso_use_rows() {
+  static const int use_rows = [] {
+    const char* e = getenv("WGCS_GSO_KERNEL");
+    return e && e[0] == 'r' ? 1 : 0;
+  }();
+  return use_rows;
+}
+
+void gso_kernel_shape(int* lds_waves, int* parts, int* u, int* rows) {
+  if (lds_waves) *lds_waves = WGCS_GSO_LDS_WAVES;
+  if (parts) *parts = WGCS_GSO_PARTS;
+  if (u) *u = WGCS_GSO_U;
+  if (rows) *rows = gso_use_rows();
+}
+
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs, uint8_t* out,
                                   uint32_t out_stride, uint32_t offset, uint32_t max_segs, int32_t* sizes,
                                   int32_t* count, int32_t* status, hipStream_t s, const GsoOutPos* outpos,
                                   uint32_t room) {
   if (n_jobs == 0 || max_segs == 0) return hipSuccess;
   if (!outpos) room = out_stride > offset ? out_stride - offset : 0;
-  // WGCS_GSO_KERNEL=rows selects the round-4 grid (A/B builds and probes)
-  static const int use_rows = [] {
-    const char* e = getenv("WGCS_GSO_KERNEL");
-    return e && e[0] == 'r' ? 1 : 0;
-  }();
+  const int use_rows = gso_use_rows();
   if (!use_rows) {
     constexpr int NW = WGCS_GSO_LDS_WAVES;
     constexpr int P = WGCS_GSO_PARTS;

@@ -17,6 +17,7 @@ hipError_t launch_checksum_batch(int mode, unsigned flags, uint8_t* arena, const
 // requests of ctl (coherent pinned host memory) until its stop word or
 // idle_ticks (100 MHz) without a request
 hipError_t launch_ring(RingCtl* ctl, uint32_t nb, uint32_t last, uint64_t idle_ticks, hipStream_t s);
+void gso_kernel_shape(int* lds_waves, int* parts, int* u, int* rows);
 hipError_t launch_gso_split_batch(const uint8_t* arena, const wgcs_gso_job* jobs, uint32_t n_jobs,
                                   uint8_t* out, uint32_t out_stride, uint32_t offset, uint32_t max_segs,
                                   int32_t* sizes, int32_t* count, int32_t* status,

@@ -8,6 +8,7 @@ Algorithmic bytes per launch = bytes read + bytes written.
 """
 from __future__ import annotations
 
+import ctypes as C
 import json
 import os
 import time
@@ -102,14 +103,22 @@ def run(args, torch, dev, dist, rank, world, local, barrier):
     elapsed = shard.max_over_ranks(elapsed, dist)
     stream = streams[0]
     achieved = bytes_per_step / (kern_ms * 1e-3) / 1e9
-    if os.environ.get("WGCS_GSO_KERNEL", "")[:1] == "r":  # the round-4 grid (A/B)
-        kname = "gso_rows_kernel<6,true>"
+    # the kernel and grid as the library was compiled (wgcs_gso_kernel_shape)
+    nw, parts, uu, rows = (C.c_int(0) for _ in range(4))
+    dev.lib.wgcs_gso_kernel_shape(C.byref(nw), C.byref(parts), C.byref(uu), C.byref(rows))
+    if rows.value:  # the round-4 grid (WGCS_GSO_KERNEL=rows, A/B)
+        kname = f"gso_rows_kernel<{uu.value},true>"
         grid = (f"({n_jobs}, {min((max_segs + 15) // 16, 3)}) blocks of 256: one block per (job, group lane), "
                 "looping over segment groups")
+    elif parts.value == 1:
+        kname = f"gso_lds_kernel<{nw.value},{uu.value},true>"
+        grid = (f"{n_jobs} blocks of {nw.value * 64}: one workgroup per read, staging it in LDS by LDS-DMA, "
+                "16-lane rows stream its segments out")
     else:
-        kname = "gso_lds_kernel<4,6,true,3>"
-        grid = (f"{(n_jobs + 7) // 8 * 8 * 3} blocks of 256: three workgroups per read (dealt to one XCD), each "
-                "staging about a third of the read in LDS by LDS-DMA, 16-lane rows stream its segments out")
+        kname = f"gso_lds_kernel<{nw.value},{uu.value},true,{parts.value}>"
+        grid = (f"{(n_jobs + 7) // 8 * 8 * parts.value} blocks of {nw.value * 64}: {parts.value} workgroups per read "
+                f"(dealt to one XCD), each staging about 1/{parts.value} of the read in LDS by LDS-DMA, 16-lane rows "
+                "stream its segments out")
     # calibration: a plain device-to-device copy of the super-packet bytes
     # (same read + write volume, same rotation) with the runtime's copy kernel
     with torch.cuda.stream(stream):
