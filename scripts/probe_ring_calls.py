@@ -55,8 +55,9 @@ pk = arena[:1500].copy()
 ppk = dev.host_alloc(1536)
 ppk[:1500] = pk
 v = C.c_int(0)
-assert ring.checksum_valid(pk, 20, 6, False) and ring.checksum_valid(ppk[:1500], 20, 6, False)
-res["checksum_valid"] = {
+SKIP_CS = os.environ.get("PROBE_SKIP_CS") == "1"  # virtio reads only (no inline requests before them)
+assert SKIP_CS or ring.checksum_valid(pk, 20, 6, False) and ring.checksum_valid(ppk[:1500], 20, 6, False)
+res["checksum_valid"] = {} if SKIP_CS else {
     "per_call_launch": med(lambda: L.wgcs_checksum_valid(h, pk.ctypes.data, 1500, 20, 6, 0, C.byref(v))),
     "ring_copied": med(lambda: L.wgcs_ring_checksum_valid(rh, pk.ctypes.data, 1500, 20, 6, 0, C.byref(v))),
     "ring_pinned": med(lambda: L.wgcs_ring_checksum_valid(rh, ppk.ctypes.data, 1500, 20, 6, 0, C.byref(v))),

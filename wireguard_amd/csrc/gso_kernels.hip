@@ -1293,62 +1293,124 @@ __device__ uint32_t ring_validate(const uint8_t* pkt, int len, int cs, int proto
   return (t == 0xFFFFu && cs <= len) ? 1u : 0u;
 }
 
+// checksumValid of an inline request from the poll's registers: lane l of
+// load j holds chunk 64 j + l, i.e. payload bytes [12 p, 12 p + 12) for
+// p = 64 j + l - 8 >= 0 in its words 1-3 (word 0 is seq).  Every word starts
+// at an offset that is a multiple of 4, so the 16-bit pairing is the
+// packet's own; bytes past what the host wrote are masked off (main range
+// [iphLen, len), addresses within the bytes carried).
+__device__ uint32_t ring_validate_inline(const u32x4s (&x)[3], int len, int cs, int proto, bool v6) {
+  const int lane = threadIdx.x & 63;
+  const int main_lo = min(cs, len), main_hi = len;
+  const int addr_lo = v6 ? 8 : 12, addr_hi = v6 ? 40 : 20;
+  const bool rot_addr = ((addr_lo ^ main_lo) & 1) != 0;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int p = 64 * j + lane - 8;
+    if (p >= 0) {
+#pragma unroll
+      for (int m = 1; m < 4; ++m) {
+        const int b0 = 12 * p + 4 * (m - 1);
+        const uint32_t w = x[j][m];
+        acc = add_halves(acc, w & expand_nibble(byte_bits16(main_lo - b0, main_hi - b0) & 0xFu));
+        uint32_t y = w & expand_nibble(byte_bits16(addr_lo - b0, addr_hi - b0) & 0xFu);
+        if (rot_addr) y = rotl8(y);
+        acc = add_halves(acc, y);
+      }
+    }
+  }
+  uint32_t s = fold32_16(wave_sum_u32(fold32_16(acc)));
+  if ((main_lo & 1) == 0) s = bswap16(s);
+  const uint32_t t = fold32_16(s + (uint32_t)proto + ((uint32_t)(len - cs) & 0xFFFFu));
+  return (t == 0xFFFFu && cs <= len) ? 1u : 0u;
+}
+
 __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0, uint64_t idle_ticks) {
-  __shared__ uint32_t s_q;
+  __shared__ uint32_t s_q, s_valid;
   __shared__ uint32_t s_w[32];  // the request record's words
   RingReq* const rq = &ctl->req;
   uint32_t last = last0;
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     if (threadIdx.x < 64) {
-      // wave 0 polls the whole 128-B record with ONE system-scope load per
-      // poll (lanes 0-7: 16 B each), so the request's fields arrive with its
-      // number -- one PCIe round trip, not one per field
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(rq, (short)0, (int)sizeof(RingReq),
+      // wave 0 polls the record and the inline payload after it with three
+      // system-scope 16-B loads per lane (chunk 64 j + lane) per poll, so the
+      // request's fields -- and an inline packet -- arrive with its number:
+      // one PCIe round trip, not one per field
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(rq, (short)0, (int)(16 * kRingPollChunks),
                                                                           0x00020000);
-      const int part = threadIdx.x & 7;
+      const int lane = threadIdx.x;
       uint32_t q = 0;
-      u32x4s v;
-      // 0: keep polling; 1: a new untorn record; 2: stop / idle deadline
-      auto check = [&](const u32x4s& x) -> int {
-        q = (uint32_t)__builtin_amdgcn_readlane((int)x[0], 0);
-        if (__builtin_amdgcn_readlane((int)x[kRqStop & 3], 0) != 0) return 2;
+      // 0: keep polling; 1: a new untorn record (and payload); 2: stop / idle deadline
+      auto check = [&](const u32x4s (&x)[3]) -> int {
+        q = (uint32_t)__builtin_amdgcn_readlane((int)x[0][0], 0);
+        if (__builtin_amdgcn_readlane((int)x[0][kRqStop & 3], 0) != 0) return 2;
         // all eight chunks carry the same new seq: an untorn record
-        const bool same = __builtin_amdgcn_ballot_w64(threadIdx.x < 8 && x[0] != q) == 0;
-        if (q != last && same) return 1;
+        const bool same = __builtin_amdgcn_ballot_w64(lane < 8 && x[0][0] != q) == 0;
+        if (q != last && same) {
+          if (blockIdx.x == 0 &&
+              (uint32_t)__builtin_amdgcn_readlane((int)x[0][kRqOp & 3], kRqOp >> 2) == kRingOpChecksumInline) {
+            // ... and every payload chunk the request carries
+            const int nch = ((int)__builtin_amdgcn_readlane((int)x[0][kRqInl & 3], kRqInl >> 2) + 11) / 12;
+            const bool torn = (lane >= 8 && lane - 8 < nch && x[0][0] != q) || (56 + lane < nch && x[1][0] != q) ||
+                              (120 + lane < nch && x[2][0] != q);
+            if (__builtin_amdgcn_ballot_w64(torn) != 0) return 0;
+          }
+          return 1;
+        }
         if (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) return 2;
         return 0;
       };
+      auto poll = [&](u32x4s (&x)[3]) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) x[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * (64 * j + lane), 0, 17);
+      };
       // two polls in flight, issued half a round trip apart: a posted request
       // is seen ~RTT/4 sooner on average than with one poll at a time
-      u32x4s va = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * part, 0, 17), vb;  // sc0 sc1
+      u32x4s va[3], vb[3], v[3];
+      poll(va);
       int st;
       for (;;) {
         __builtin_amdgcn_s_sleep(1);
-        vb = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * part, 0, 17);
+        poll(vb);
         if ((st = check(va)) != 0) {
-          v = va;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) v[j] = va[j];
           break;
         }
         __builtin_amdgcn_s_sleep(1);
-        va = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * part, 0, 17);
+        poll(va);
         if ((st = check(vb)) != 0) {
-          v = vb;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) v[j] = vb[j];
           break;
         }
       }
       if (st == 2) q = 0xFFFFFFFFu;
-      if (threadIdx.x < 8) {
-        s_w[4 * part] = v[0];
-        s_w[4 * part + 1] = v[1];
-        s_w[4 * part + 2] = v[2];
-        s_w[4 * part + 3] = v[3];
+      if (lane < 8) {
+        s_w[4 * lane] = v[0][0];
+        s_w[4 * lane + 1] = v[0][1];
+        s_w[4 * lane + 2] = v[0][2];
+        s_w[4 * lane + 3] = v[0][3];
       }
-      if (threadIdx.x == 0) s_q = q;
+      uint32_t iv = 0;
+      if (st == 1 && blockIdx.x == 0 &&
+          (uint32_t)__builtin_amdgcn_readlane((int)v[0][kRqOp & 3], kRqOp >> 2) == kRingOpChecksumInline) {
+        auto f = [&](uint32_t k) { return __builtin_amdgcn_readlane((int)v[0][k & 3], (int)(k >> 2)); };
+        iv = ring_validate_inline(v, f(kRqLen), f(kRqCs), f(kRqProto), (f(kRqFlags) & WGCS_PKT_V6) != 0);
+      }
+      if (lane == 0) {
+        s_q = q;
+        s_valid = iv;
+      }
     }
     __syncthreads();
     const uint32_t q = s_q;
     if (q == 0xFFFFFFFFu) break;  // block-uniform: every wave leaves
+#ifdef WGCS_RING_STAMPS  // probe builds: s_memrealtime stamps of the request's phases
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+#endif
     auto w = [&](uint32_t k) { return (uint32_t)ufl((int)s_w[k]); };
     auto p64 = [&](uint32_t lo, uint32_t hi) { return (uint64_t)w(lo) | ((uint64_t)w(hi) << 32); };
     // request pointers as global-address-space ones: the inlined body then
@@ -1357,7 +1419,9 @@ __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0,
     auto gptr = [&](uint32_t lo, uint32_t hi) { return (uint8_t*)(g8*)(uintptr_t)p64(lo, hi); };
     const uint32_t op = w(kRqOp);
     uint32_t valid = 0;
-    if (op == kRingOpChecksumValid) {
+    if (op == kRingOpChecksumInline) {
+      valid = s_valid;  // workgroup 0's wave 0 checked it from the poll's registers
+    } else if (op == kRingOpChecksumValid) {
       if (blockIdx.x == 0 && threadIdx.x < 64)
         valid = ring_validate(gptr(kRqPktLo, kRqPktHi), (int)w(kRqLen),
                               (int)w(kRqCs), (int)w(kRqProto), (w(kRqFlags) & WGCS_PKT_V6) != 0);
@@ -1373,13 +1437,28 @@ __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0,
     // releases them at system scope (the fence's own wait made explicit:
     // MI355X_MICROARCH.md); then {seq, valid} in ONE 8-byte write-through
     // store on this workgroup's own line, which the host spins on
+#ifdef WGCS_RING_STAMPS
+    const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
+#ifdef WGCS_RING_STAMPS
+      const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifndef WGCS_RING_NOFENCE  // A/B builds: timing without the system-scope release (not exact output)
       if (op == kRingOpVirtioRead) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+#endif
+#ifdef WGCS_RING_STAMPS
+      {  // {body issued, drained, released, idle before} in 10-ns ticks from the request's start
+        const uint64_t t4 = __builtin_amdgcn_s_memrealtime();
+        const u32x4s st = {(uint32_t)(t2 - t1), (uint32_t)(t3 - t1), (uint32_t)(t4 - t1), (uint32_t)(t1 - t_last)};
+        const __amdgpu_buffer_rsrc_t ss = __builtin_amdgcn_make_buffer_rsrc(&ctl->dn[blockIdx.x], (short)0, 64,
+                                                                            0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(st, ss, 16, 0, 17);
       }
 #endif
       typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));

@@ -22,7 +22,9 @@
 // out (gso_api.cpp's post-processing), so every byte matches the per-call path.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -71,6 +73,16 @@ int grow_coherent(wgcs_ctx* ctx, uint8_t** p, size_t* cap, size_t want) {
 }
 
 uint32_t load_acq(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+
+// WGCS_RING_INLINE=0: checksumValid requests pass a pointer to the packet
+// instead of carrying its bytes (A/B measurements)
+bool ring_inline_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("WGCS_RING_INLINE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 int launch(wgcs_ring* rg, uint32_t last) {
   hipSetDevice(rg->ctx->device);
@@ -240,6 +252,17 @@ int wgcs_ring_info(wgcs_ring* rg, uint64_t* requests, uint64_t* launches, int* r
   return WGCS_OK;
 }
 
+#ifdef WGCS_RING_STAMPS
+// probe builds only (not in include/wgcsum.h): the last request's phase stamps
+// of workgroup b, 4 words (ring_kernel, WGCS_RING_STAMPS)
+int wgcs_ring_debug_stamps(wgcs_ring* rg, int b, uint32_t* out) {
+  if (!rg || b < 0 || b >= (int)wgcs::kRingMaxBlocks || !out) return WGCS_ERR_INVALID_ARG;
+  const volatile uint32_t* d = reinterpret_cast<const volatile uint32_t*>(&rg->ctl->dn[b]);
+  for (int i = 0; i < 4; ++i) out[i] = d[4 + i];
+  return WGCS_OK;
+}
+#endif
+
 // checksumValid through the ring: wgcs_checksum_valid_cap's arguments and errors.
 int wgcs_ring_checksum_valid_cap(wgcs_ring* rg, const uint8_t* pkt, size_t len, size_t cap, uint8_t iph_len,
                                  uint8_t proto, int is_v6, int* valid) {
@@ -250,18 +273,37 @@ int wgcs_ring_checksum_valid_cap(wgcs_ring* rg, const uint8_t* pkt, size_t len, 
     return set_err(ctx, WGCS_ERR_OUT_OF_RANGE, "pkt[%u:] or its addresses past the slice", (unsigned)iph_len);
   if (len >= 0x80000000u) return set_err(ctx, WGCS_ERR_INVALID_ARG, "packet too large");
   std::lock_guard<std::mutex> g(rg->mu);
-  const uint8_t* p = nullptr;
-  int rc = ring_input(rg, pkt, std::max(len, need), &p);
-  if (rc) return rc;
   RingReq* rq = &rg->ctl->req;
-  rq_put(rq, kRqOp, kRingOpChecksumValid);
-  rq_put64(rq, kRqPktLo, kRqPktHi, p);
+  const size_t nbytes = std::max(len, need);  // what checksumValid reads
+  int rc;
+  if (nbytes <= kRingInlineMax && ring_inline_enabled()) {
+    // the bytes travel with the request: chunk c = {seq, pkt[12c, 12c + 12)},
+    // seq stored after the data, so a chunk read with the new seq holds them
+    const uint32_t q = rg->seq + 1;  // post_and_wait's number for this request
+    const uint32_t nch = (uint32_t)((nbytes + 11) / 12);
+    for (uint32_t c = 0; c < nch; ++c) {
+      uint32_t w[3] = {0, 0, 0};
+      const size_t o = 12 * (size_t)c;
+      memcpy(w, pkt + o, std::min<size_t>(12, nbytes - o));
+      uint32_t* ch = rg->ctl->inl[c];
+      for (int k = 0; k < 3; ++k) __atomic_store_n(&ch[1 + k], w[k], __ATOMIC_RELAXED);
+      __atomic_store_n(&ch[0], q, __ATOMIC_RELEASE);
+    }
+    rq_put(rq, kRqOp, kRingOpChecksumInline);
+    rq_put(rq, kRqInl, (uint32_t)nbytes);
+  } else {
+    const uint8_t* p = nullptr;
+    if ((rc = ring_input(rg, pkt, nbytes, &p))) return rc;
+    rq_put(rq, kRqOp, kRingOpChecksumValid);
+    rq_put64(rq, kRqPktLo, kRqPktHi, p);
+  }
   rq_put(rq, kRqLen, (uint32_t)len);
   rq_put(rq, kRqCs, iph_len);
   rq_put(rq, kRqProto, proto);
   rq_put(rq, kRqFlags, is_v6 ? WGCS_PKT_V6 : 0u);
   if ((rc = post_and_wait(rg, 1))) return rc;
   *valid = (int)__atomic_load_n(&rg->ctl->dn[0].valid, __ATOMIC_ACQUIRE);
+
   return WGCS_OK;
 }
 

@@ -46,7 +46,7 @@ struct GsoOutPos {
 // request record the host fills and then publishes by storing `seq` last, and
 // the device's completion record on a line of its own; both in fine-grained
 // (coherent) pinned host memory.
-enum : uint32_t { kRingOpChecksumValid = 1, kRingOpVirtioRead = 2 };
+enum : uint32_t { kRingOpChecksumValid = 1, kRingOpVirtioRead = 2, kRingOpChecksumInline = 3 };
 // The request record: eight 16-byte chunks, each {seq, 3 fields}.  The host
 // stores the fields, then seq into every chunk (x86 stores become visible in
 // order); the GPU reads the record with ONE wave load (lane k: chunk k) and
@@ -65,7 +65,14 @@ enum : uint32_t {
   kRqKbufs = 4 * 4 + 1, kRqPitch = 4 * 4 + 2, kRqRoom = 4 * 4 + 3,     // slots, segment pitch, bufs[0] room
   kRqPosFlags = 5 * 4 + 1, kRqOutLo = 5 * 4 + 2, kRqOutHi = 5 * 4 + 3, // kOutPosTails; segment i at out + i pitch
   kRqMetaLo = 6 * 4 + 1, kRqMetaHi = 6 * 4 + 2,                        // int32 sizes[kbufs] | count | status
+  kRqInl = kRqVlen,                                                    // inline checksumValid: bytes carried
 };
+// Inline checksumValid: the packet's bytes travel with the request, 12 per
+// 16-byte chunk {seq, 3 data words} right after the record, so the poll that
+// finds the request already holds them (one PCIe round trip fewer than reading
+// pkt).  One poll reads kRingPollChunks chunks (wave 0: three 16-B loads per
+// lane); the record takes 8 of them.
+enum : uint32_t { kRingPollChunks = 192, kRingInlineChunks = kRingPollChunks - 8, kRingInlineMax = kRingInlineChunks * 12 };
 // One per workgroup, each on a 64-B line of its own: {seq, valid} is written
 // by ONE 8-byte write-through store after the request's results.
 struct RingDone {
@@ -77,10 +84,13 @@ struct RingDone {
 enum : uint32_t { kRingMaxBlocks = 8 };
 struct RingCtl {
   RingReq req;
+  uint32_t inl[kRingInlineChunks][4];  // inline payload chunks (follow req: one poll reads both)
   uint32_t pad[16];
   RingDone dn[kRingMaxBlocks];
 };
-static_assert(sizeof(RingReq) % 64 == 0 && offsetof(RingCtl, dn) % 64 == 0 && sizeof(RingDone) == 64,
+static_assert(sizeof(RingReq) % 64 == 0 && offsetof(RingCtl, dn) % 64 == 0 && sizeof(RingDone) == 64 &&
+                  offsetof(RingCtl, inl) == sizeof(RingReq) && sizeof(RingReq) + sizeof(((RingCtl*)0)->inl) ==
+                                                                   16 * kRingPollChunks,
               "the records on lines of their own");
 
 // Packed-layout pitch and segment bound of one job ([10-byte virtio header |
