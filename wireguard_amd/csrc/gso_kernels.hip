@@ -1012,11 +1012,19 @@ __device__ __noinline__ int decoded_rows(const uint8_t* vb_a, uint32_t jlen_a, u
 // per job takes the job's segment groups by, by + gy, ...  The descriptor and
 // output position come by value (the resident ring kernel passes a request's,
 // gso_rows_kernel its grid's); `has_pos`: use pos, else fixed slots.
+// 16 bytes at a 4-byte aligned generic pointer that points into LDS (ds reads)
+__device__ __forceinline__ uint4 lds16_a4(const uint8_t* p) {
+  typedef __attribute__((address_space(3))) const uint32_t l32;
+  const l32* q = (const l32*)(const __attribute__((address_space(3))) uint8_t*)p;
+  return make_uint4(q[0], q[1], q[2], q[3]);
+}
+
 template <int U, bool NT>
 __device__ __forceinline__ void gso_rows_body(const uint8_t* arena, const wgcs_gso_job job, uint32_t jb, int by,
                                               int gy, uint32_t max_segs, uint8_t* out, uint32_t out_stride,
                                               bool has_pos, const GsoOutPos pos, uint32_t offset, uint32_t room,
-                                              int32_t* sizes, int32_t* count, int32_t* status) {
+                                              int32_t* sizes, int32_t* count, int32_t* status,
+                                              const uint8_t* hlds = nullptr) {
   constexpr int ROWS = 16;
 #ifdef WGCS_GSO_STAMPS  // timing-only build (scripts/probe_gso_stamps.py): s_memrealtime per wave phase
   uint64_t stp[5] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0};
@@ -1049,7 +1057,9 @@ __device__ __forceinline__ void gso_rows_body(const uint8_t* arena, const wgcs_g
   const uint8_t* hbase = rb - hph;
   const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t*>(hbase), (short)0, (int)(jlen + 3u) - (int)(hbase - vb), 0x00020000);
-  const uint4 H0 = bld16<false>(hrs, 16 * r);
+  // (hlds: the resident ring's copy of vb[0, 272) in LDS, vb[k] at hlds[k],
+  // same phase mod 16 as vb -- the header without a host-memory round trip)
+  const uint4 H0 = hlds ? lds16_a4(hlds + (hbase - vb) + 16 * r) : bld16<false>(hrs, 16 * r);
 
   // ---- virtio header + the IP version byte: 16 bytes from the dword below
   // vb, one wave-uniform load (readable: jlen >= 14 and the arena contract)
@@ -1060,8 +1070,10 @@ __device__ __forceinline__ void gso_rows_body(const uint8_t* arena, const wgcs_g
     const int sh = (int)((uintptr_t)vb & 3u);
     // a range-checked vector load (zeros past the job), not a scalar one: the
     // resident ring kernel reads requests that change at the same address
-    const uint4 w = bld16<false>(__builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vb - sh), (short)0,
-                                                                 (int)(jlen + 3u + (uint32_t)sh), 0x00020000), 0);
+    const uint4 w = hlds ? lds16_a4(hlds - sh)
+                         : bld16<false>(__builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vb - sh), (short)0,
+                                                                          (int)(jlen + 3u + (uint32_t)sh), 0x00020000),
+                                        0);
     const uint64_t lo = ((uint64_t)w.y << 32) | w.x, hi = ((uint64_t)w.w << 32) | w.z;
     // bytes [sh, sh + 11) of the 16: the virtio header and readBuf[0]
     const uint64_t v0 = sh ? (lo >> (8 * sh)) | (hi << (64 - 8 * sh)) : lo;  // vb[0..8)
@@ -1329,6 +1341,7 @@ __device__ uint32_t ring_validate_inline(const u32x4s (&x)[3], int len, int cs, 
 __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0, uint64_t idle_ticks) {
   __shared__ uint32_t s_q, s_valid;
   __shared__ uint32_t s_w[32];  // the request record's words
+  __shared__ __attribute__((aligned(16))) uint32_t s_hdr[3 * kRingHdrChunks];  // a virtio read's first bytes
   RingReq* const rq = &ctl->req;
   uint32_t last = last0;
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
@@ -1349,10 +1362,15 @@ __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0,
         // all eight chunks carry the same new seq: an untorn record
         const bool same = __builtin_amdgcn_ballot_w64(lane < 8 && x[0][0] != q) == 0;
         if (q != last && same) {
-          if (blockIdx.x == 0 &&
-              (uint32_t)__builtin_amdgcn_readlane((int)x[0][kRqOp & 3], kRqOp >> 2) == kRingOpChecksumInline) {
+          const uint32_t op = (uint32_t)__builtin_amdgcn_readlane((int)x[0][kRqOp & 3], kRqOp >> 2);
+          const uint32_t nin =
+              (blockIdx.x == 0 && op == kRingOpChecksumInline)
+                  ? (uint32_t)__builtin_amdgcn_readlane((int)x[0][kRqInl & 3], kRqInl >> 2)
+              : op == kRingOpVirtioRead ? (uint32_t)__builtin_amdgcn_readlane((int)x[0][kRqHdrInl & 3], kRqHdrInl >> 2)
+                                        : 0u;
+          if (nin != 0) {
             // ... and every payload chunk the request carries
-            const int nch = ((int)__builtin_amdgcn_readlane((int)x[0][kRqInl & 3], kRqInl >> 2) + 11) / 12;
+            const int nch = ((int)nin + 11) / 12;
             const bool torn = (lane >= 8 && lane - 8 < nch && x[0][0] != q) || (56 + lane < nch && x[1][0] != q) ||
                               (120 + lane < nch && x[2][0] != q);
             if (__builtin_amdgcn_ballot_w64(torn) != 0) return 0;
@@ -1394,6 +1412,17 @@ __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0,
         s_w[4 * lane + 2] = v[0][2];
         s_w[4 * lane + 3] = v[0][3];
       }
+      // a virtio read's inline header bytes into LDS (zeros past them): word
+      // 3p + m - 1 = chunk p's word m, the buffer's phase mod 16 kept
+      if (st == 1 && (uint32_t)__builtin_amdgcn_readlane((int)v[0][kRqOp & 3], kRqOp >> 2) == kRingOpVirtioRead) {
+        const int nch = ((int)__builtin_amdgcn_readlane((int)v[0][kRqHdrInl & 3], kRqHdrInl >> 2) + 11) / 12;
+        const int p = lane - 8;
+        if (p >= 0 && p < (int)kRingHdrChunks) {
+          s_hdr[3 * p] = p < nch ? v[0][1] : 0u;
+          s_hdr[3 * p + 1] = p < nch ? v[0][2] : 0u;
+          s_hdr[3 * p + 2] = p < nch ? v[0][3] : 0u;
+        }
+      }
       uint32_t iv = 0;
       if (st == 1 && blockIdx.x == 0 &&
           (uint32_t)__builtin_amdgcn_readlane((int)v[0][kRqOp & 3], kRqOp >> 2) == kRingOpChecksumInline) {
@@ -1430,8 +1459,11 @@ __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0,
       const GsoOutPos pos = {0, w(kRqPitch), w(kRqPosFlags)};
       int32_t* h = (int32_t*)(__attribute__((address_space(1))) int32_t*)(uintptr_t)p64(kRqMetaLo, kRqMetaHi);
       const uint32_t kb = w(kRqKbufs);
-      gso_rows_body<WGCS_GSO_U, false>(gptr(kRqVbufLo, kRqVbufHi), job, 0, (int)blockIdx.x, (int)gridDim.x, kb,
-                                       gptr(kRqOutLo, kRqOutHi), 0, true, pos, 0, w(kRqRoom), h, h + kb, h + kb + 1);
+      const uint8_t* vb = gptr(kRqVbufLo, kRqVbufHi);
+      // the inline header: vb[k] at LDS byte (vb & 15) + k
+      const uint8_t* hl = w(kRqHdrInl) ? reinterpret_cast<const uint8_t*>(s_hdr) + ((uintptr_t)vb & 15u) : nullptr;
+      gso_rows_body<WGCS_GSO_U, false>(vb, job, 0, (int)blockIdx.x, (int)gridDim.x, kb, gptr(kRqOutLo, kRqOutHi), 0,
+                                       true, pos, 0, w(kRqRoom), h, h + kb, h + kb + 1, hl);
     }
     // completion: every wave's stores done; a request that stored results
     // releases them at system scope (the fence's own wait made explicit:

@@ -100,6 +100,20 @@ void rq_put64(RingReq* rq, uint32_t lo, uint32_t hi, const void* p) {
   rq_put(rq, hi, (uint32_t)((uint64_t)(uintptr_t)p >> 32));
 }
 
+// Inline bytes of the next request: chunk c = {seq, src[12c, 12c + 12)}
+// (zeros past n), seq stored after the data, so a chunk read with the new
+// seq holds them.
+void ring_put_inline(wgcs_ring* rg, const uint8_t* src, uint32_t n) {
+  const uint32_t q = rg->seq + 1;  // post_and_wait's number for this request
+  for (uint32_t c = 0; c < (n + 11) / 12; ++c) {
+    uint32_t w[3] = {0, 0, 0};
+    memcpy(w, src + 12 * c, std::min<uint32_t>(12, n - 12 * c));
+    uint32_t* ch = rg->ctl->inl[c];
+    for (int k = 0; k < 3; ++k) __atomic_store_n(&ch[1 + k], w[k], __ATOMIC_RELAXED);
+    __atomic_store_n(&ch[0], q, __ATOMIC_RELEASE);
+  }
+}
+
 // workgroups [0, nb) have finished request q
 bool served(wgcs_ring* rg, uint32_t q, uint32_t nb) {
   for (uint32_t b = 0; b < nb; ++b)
@@ -166,6 +180,16 @@ int ring_gso_prepare(wgcs_ring* rg, uint32_t kbufs, size_t region, uint8_t** hs,
 int ring_gso(wgcs_ring* rg, const uint8_t* vbuf, uint32_t vlen, uint32_t jflags, uint32_t kbufs, uint32_t pitch,
              uint32_t room, uint32_t posflags, uint8_t* out, int32_t* meta) {
   RingReq* rq = &rg->ctl->req;
+  uint32_t hin = 0;  // inline header bytes (with the phase padding)
+  if (ring_inline_enabled()) {
+    const uint32_t ph = (uint32_t)((uintptr_t)vbuf & 15u);
+    const uint32_t n = vlen < kRingHdrBytes ? vlen : kRingHdrBytes;
+    hin = ph + n;
+    uint8_t tmp[16 + kRingHdrBytes] = {};
+    memcpy(tmp + ph, vbuf, n);
+    ring_put_inline(rg, tmp, hin);
+  }
+  rq_put(rq, kRqHdrInl, hin);
   rq_put(rq, kRqOp, kRingOpVirtioRead);
   rq_put64(rq, kRqVbufLo, kRqVbufHi, vbuf);
   rq_put(rq, kRqVlen, vlen);
@@ -279,16 +303,7 @@ int wgcs_ring_checksum_valid_cap(wgcs_ring* rg, const uint8_t* pkt, size_t len, 
   if (nbytes <= kRingInlineMax && ring_inline_enabled()) {
     // the bytes travel with the request: chunk c = {seq, pkt[12c, 12c + 12)},
     // seq stored after the data, so a chunk read with the new seq holds them
-    const uint32_t q = rg->seq + 1;  // post_and_wait's number for this request
-    const uint32_t nch = (uint32_t)((nbytes + 11) / 12);
-    for (uint32_t c = 0; c < nch; ++c) {
-      uint32_t w[3] = {0, 0, 0};
-      const size_t o = 12 * (size_t)c;
-      memcpy(w, pkt + o, std::min<size_t>(12, nbytes - o));
-      uint32_t* ch = rg->ctl->inl[c];
-      for (int k = 0; k < 3; ++k) __atomic_store_n(&ch[1 + k], w[k], __ATOMIC_RELAXED);
-      __atomic_store_n(&ch[0], q, __ATOMIC_RELEASE);
-    }
+    ring_put_inline(rg, pkt, (uint32_t)nbytes);
     rq_put(rq, kRqOp, kRingOpChecksumInline);
     rq_put(rq, kRqInl, (uint32_t)nbytes);
   } else {

@@ -65,6 +65,7 @@ enum : uint32_t {
   kRqKbufs = 4 * 4 + 1, kRqPitch = 4 * 4 + 2, kRqRoom = 4 * 4 + 3,     // slots, segment pitch, bufs[0] room
   kRqPosFlags = 5 * 4 + 1, kRqOutLo = 5 * 4 + 2, kRqOutHi = 5 * 4 + 3, // kOutPosTails; segment i at out + i pitch
   kRqMetaLo = 6 * 4 + 1, kRqMetaHi = 6 * 4 + 2,                        // int32 sizes[kbufs] | count | status
+  kRqHdrInl = 6 * 4 + 3,                                               // virtio read: inline header bytes (0: none)
   kRqInl = kRqVlen,                                                    // inline checksumValid: bytes carried
 };
 // Inline checksumValid: the packet's bytes travel with the request, 12 per
@@ -72,7 +73,12 @@ enum : uint32_t {
 // finds the request already holds them (one PCIe round trip fewer than reading
 // pkt).  One poll reads kRingPollChunks chunks (wave 0: three 16-B loads per
 // lane); the record takes 8 of them.
+// A handleVirtioRead request carries the first bytes of its readBuf the same
+// way (kRingHdrBytes, behind vbuf & 15 bytes of padding so that their phase
+// mod 16 is the buffer's): the header decode and the verdict start from them
+// while the payload loads go out.
 enum : uint32_t { kRingPollChunks = 192, kRingInlineChunks = kRingPollChunks - 8, kRingInlineMax = kRingInlineChunks * 12 };
+enum : uint32_t { kRingHdrBytes = 272, kRingHdrChunks = (15 + kRingHdrBytes + 11) / 12 };  // 24 chunks, 288 B
 // One per workgroup, each on a 64-B line of its own: {seq, valid} is written
 // by ONE 8-byte write-through store after the request's results.
 struct RingDone {
