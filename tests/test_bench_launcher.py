@@ -137,20 +137,25 @@ def test_recorded_rehearsal_lines_complete():
                     assert bench.line_problems(line, require_cold=not pre6) == [], fn
 
 
-def test_recorded_eight_rank_rehearsal():
+@pytest.mark.parametrize("rnd", ["r5", "r6"])
+def test_recorded_eight_rank_rehearsal(rnd):
     """the driver's 8-GPU run is one-shot, so the 8-rank
     line was rehearsed once on the 1-GPU box (`WGCS_DIST_BACKEND=gloo python
     bench.py --gpus 8 --steps 20 --warmup 5`, 8 gloo ranks time-sharing
-    cuda:0, profiles/r5_rehearse_gpus8_gloo.jsonl): one complete line, every
-    rank's kernel time, the 1M batch split over all 8, and rank 0's CPU
-    baseline inside the run the other 7 ranks waited for at the barrier."""
-    fn = os.path.join(ROOT, "profiles", "r5_rehearse_gpus8_gloo.jsonl")
+    cuda:0, profiles/r5_rehearse_gpus8_gloo.jsonl; again with round 6's
+    bench, cfg5_strong.value_cold included): one complete
+    line, every rank's kernel time, the 1M batch split over all 8, and rank
+    0's CPU baseline inside the run the other 7 ranks waited for at the
+    barrier."""
+    fn = os.path.join(ROOT, "profiles", f"{rnd}_rehearse_gpus8_gloo.jsonl")
     if not os.path.exists(fn):
         pytest.skip("8-rank rehearsal not recorded yet")
     lines = [json.loads(l) for l in open(fn) if l.startswith("{")]
     assert len(lines) == 1
     line = lines[0]
-    assert bench.line_problems(line, require_cold=False) == []
+    assert bench.line_problems(line, require_cold=rnd != "r5") == []
+    if rnd != "r5":
+        assert line["cfg5_strong"]["value_cold"] == line["cfg5_strong"]["value"]
     assert line["n_gpus"] == 8 and line["config"]["dist"]["world_size"] == 8
     assert len(line["roofline"]["kernel_ms_per_rank"]) == 8
     assert len(line["cfg5_strong"]["packets_per_rank"]) == 8
