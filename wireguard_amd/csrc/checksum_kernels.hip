@@ -40,19 +40,25 @@ struct Ranges {
 
 // Masked contribution of an edge chunk (head: addresses / gap / field; tail)
 // at packet position `pos`.
-__device__ __forceinline__ uint32_t edge_chunk(uint32_t acc, const uint4& v, int pos, const Ranges& r, bool rot_addr) {
+// `addr`: wave-uniform, false when no packet of the wave has a separate
+// address range (merged into the main range, below): the second mask is skipped.
+__device__ __forceinline__ uint32_t edge_chunk(uint32_t acc, const uint4& v, int pos, const Ranges& r, bool rot_addr,
+                                               bool addr) {
   const int f = r.fld - pos;
   uint32_t fb = 0;
   if (f >= -1 && f < 16) fb = ((3u << (f + 1)) >> 1) & 0xFFFFu;
   const uint32_t m16 = byte_bits16(r.main_lo - pos, r.main_hi - pos) & ~fb;
-  const uint32_t a16 = byte_bits16(r.addr_lo - pos, r.addr_hi - pos) & ~fb;  // the field is zeroed memory
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    acc = add_halves(acc, w[k] & expand_nibble((m16 >> (4 * k)) & 0xFu));
-    uint32_t y = w[k] & expand_nibble((a16 >> (4 * k)) & 0xFu);
-    if (rot_addr) y = rotl8(y);  // 256*y (mod 2^32-1): address pairing parity differs from the main range
-    acc = add_halves(acc, y);
+  for (int k = 0; k < 4; ++k) acc = add_halves(acc, w[k] & expand_nibble((m16 >> (4 * k)) & 0xFu));
+  if (addr) {
+    const uint32_t a16 = byte_bits16(r.addr_lo - pos, r.addr_hi - pos) & ~fb;  // the field is zeroed memory
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t y = w[k] & expand_nibble((a16 >> (4 * k)) & 0xFu);
+      if (rot_addr) y = rotl8(y);  // 256*y (mod 2^32-1): address pairing parity differs from the main range
+      acc = add_halves(acc, y);
+    }
   }
   return acc;
 }
@@ -108,6 +114,9 @@ __device__ __forceinline__ uint4 wave_desc(const uint4* __restrict__ pkts, uint3
 
 #ifndef WGCS_CS_ACC2
 #define WGCS_CS_ACC2 1  // two accumulator chains per lane (0: one, round 5)
+#endif
+#ifndef WGCS_CS_MERGE
+#define WGCS_CS_MERGE 1  // contiguous address + summed ranges as one (0: two masks per edge chunk, round 5)
 #endif
 #ifndef WGCS_CS_BLOCK
 #define WGCS_CS_BLOCK 256  // threads per block (A/B builds: 512, 1024)
@@ -169,6 +178,16 @@ __global__ __launch_bounds__(WGCS_CS_BLOCK) void checksum_batch_kernel(uint8_t* 
       r.main_hi = min(cs, len);
       r.fld = 10;
     }
+#if WGCS_CS_MERGE
+    // pseudo-header addresses that end where the summed range starts (iphLen
+    // 20 / 40, the usual case) pair the same way: one range [addr_lo, len)
+    // with one mask, and from there no gap to mask (round 6)
+    if (r.addr_hi > r.addr_lo && r.addr_hi == r.main_lo && ((r.addr_lo ^ r.main_lo) & 1) == 0) {
+      r.main_lo = r.addr_lo;
+      r.addr_lo = r.addr_hi = 0;
+    }
+#endif
+    const bool any_addr = __builtin_amdgcn_ballot_w64(r.addr_hi > r.addr_lo) != 0;  // wave-uniform
     const uintptr_t pbase = (uintptr_t)pkt;
     const bool rot_addr = (((pbase + r.addr_lo) ^ (pbase + r.main_lo)) & 1u) != 0;
     int lo_all = r.main_lo, hi_all = r.main_hi, hole_end = r.main_lo;
@@ -210,7 +229,7 @@ __global__ __launch_bounds__(WGCS_CS_BLOCK) void checksum_batch_kernel(uint8_t* 
       }
       if (edge_pending) {
         for (int e = sub;;) {  // rows with more than G edge chunks (long field offsets) loop
-          if (e < n_edge) acc = edge_chunk(acc, ve, rel0 + 16 * ce, r, rot_addr);
+          if (e < n_edge) acc = edge_chunk(acc, ve, rel0 + 16 * ce, r, rot_addr, any_addr);
           e += G;
           if (e >= n_edge) break;
           ce = e < c_lo ? e : c_hi + (e - c_lo);

@@ -84,8 +84,12 @@ __device__ __forceinline__ uint32_t add_halves(uint32_t acc, uint32_t w) {
 }
 
 // Expand a 4-bit byte mask into a 32-bit byte mask (bit j -> byte j = 0xFF).
+// t = one bit per byte; then v_perm_b32 with selector byte 0x0C (-> 0x00) or
+// 0x0D (-> 0xFF), not t * 255, which the compiler emits as a quarter-rate
+// 32-bit multiply (nib * 0x204081 fits the full-rate 24-bit one)
 __device__ __forceinline__ uint32_t expand_nibble(uint32_t nib) {
-  return ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;
+  const uint32_t t = (nib * 0x00204081u) & 0x01010101u;
+  return __builtin_amdgcn_perm(0u, 0u, t | 0x0C0C0C0Cu);
 }
 
 }  // namespace wgcs
