@@ -2,8 +2,9 @@
 """cfg4's access-pattern ceiling (NOT product code): the
 product's gso_lds_kernel and scripts/probe_gso_copy.hip (the same in -> out
 byte mapping as 16-byte row copies and nothing else) on the bench's batch --
-256 reads of 65,545 B, 45 segments each into 128 slots of 1,536 B at offset 16,
-8 rotated copies -- K launches on one stream and on four, HIP events, the
+256 reads of 65,545 B at 128-byte multiples, 45 segments each into 128 slots of
+1,536 B with bufs[i][16] on a 128-byte line (the bench's --gso-in-align /
+--gso-out-align defaults), 8 rotated copies -- K launches on one stream and on four, HIP events, the
 same algorithmic bytes (bytes read + bytes written).  One JSON line per
 (kernel, streams); the copy's output is checked once against the product's
 segments (the bytes it moves must be the ones the product writes, headers
@@ -33,15 +34,17 @@ K = int(os.environ.get("K", "200"))
 n_jobs, total, gso, max_segs, stride, offset, R = 256, 65535, 1460, 128, 1536, 16, 8
 pkts = [synth.make_super_packet(total, gso, seed=synth.SEED + k) for k in range(n_jobs)]
 jlen = len(pkts[0])
-arena = np.zeros(n_jobs * jlen + 64, np.uint8)
+jpitch = -(-jlen // 128) * 128
+oshift = (128 - offset % 128) % 128
+arena = np.zeros(n_jobs * jpitch + 64, np.uint8)
 for k, p in enumerate(pkts):
-    arena[k * jlen: (k + 1) * jlen] = np.frombuffer(p, np.uint8)
+    arena[k * jpitch: k * jpitch + jlen] = np.frombuffer(p, np.uint8)
 jobs = np.zeros(n_jobs, GSO_JOB_DTYPE)
-jobs["off"] = np.arange(n_jobs, dtype=np.uint64) * np.uint64(jlen)
+jobs["off"] = np.arange(n_jobs, dtype=np.uint64) * np.uint64(jpitch)
 jobs["len"] = jlen
 d_arena = [torch.from_numpy(arena).cuda() for _ in range(R)]
 d_jobs = torch.from_numpy(jobs.view(np.uint8)).cuda()
-d_out = [torch.zeros(n_jobs * max_segs * stride + 256, dtype=torch.uint8, device="cuda") for _ in range(R)]
+d_out = [torch.zeros(n_jobs * max_segs * stride + 256, dtype=torch.uint8, device="cuda")[oshift:] for _ in range(R)]
 sts = [torch.cuda.Stream() for _ in range(4)]
 d_sizes = [torch.zeros(n_jobs * max_segs, dtype=torch.int32, device="cuda") for _ in range(4)]
 d_count = [torch.zeros(n_jobs, dtype=torch.int32, device="cuda") for _ in range(4)]
@@ -54,7 +57,7 @@ def product(k, q):
 
 
 def copy(k, q):
-    rc = P.probe_gso_copy(d_arena[k % R].data_ptr(), jlen, jlen, n_jobs, d_out[k % R].data_ptr(), stride, offset,
+    rc = P.probe_gso_copy(d_arena[k % R].data_ptr(), jpitch, jlen, n_jobs, d_out[k % R].data_ptr(), stride, offset,
                           max_segs, sts[q].cuda_stream)
     assert rc == 0, rc
 
