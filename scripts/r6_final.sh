@@ -90,6 +90,11 @@ if want pmc; then
     pmcrun pmc${p%%:*}_udpsplit ${p#*:} -- $ROOT/bench.py --config udp_split --steps 10 --warmup 2 --cpu-seconds 0 --no-e2e --no-event-timing --streams 1
   done
 fi
+if want pmccs; then
+  for p in "f:FETCH_SIZE" "w:WRITE_SIZE" "s:$SIZED"; do
+    pmcrun pmc${p%%:*}_cfg2 ${p#*:} -- $ROOT/bench.py --steps 30 --warmup 3 --no-strong --cpu-seconds 0 --no-e2e --no-event-timing --streams 1
+  done
+fi
 if want gloo8; then
   export WGCS_DIST_BACKEND=gloo
   step gloo8 600 python bench.py --gpus 8 --steps 20 --warmup 5
