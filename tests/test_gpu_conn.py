@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle
-from conn_cases import Msg, clone_msgs, coalesce_case, split_case
+from conn_cases import Msg, clone_msgs, coalesce_case, gro_cmsg, split_case
 from wireguard_amd import conn
 
 pytestmark = pytest.mark.gpu
@@ -85,16 +85,10 @@ def _split_batch_ref(msgs_list, first):
     return outs
 
 
-@pytest.mark.parametrize("seed,in_stride", [(0, 65536), (1, 65536), (2, 65536), (3, 65541), (4, 65664 + 56)])
-def test_split_messages_batch(dev, seed, in_stride):
-    """Landing slots on 128-B lines and off them (odd strides): the rows that
-    share a source line through LDS see every phase of it."""
+def _split_batch_check(dev, cases, n_msgs, first, buf_len, in_stride):
     import torch
 
-    rng = np.random.default_rng(7000 + seed)
-    B, n_msgs, buf_len = 16, 128, 65535
-    first = 126
-    cases = [split_case(rng, n_msgs=n_msgs, first=first, buf_len=buf_len)[0] for _ in range(B)]
+    B = len(cases)
     ns = n_msgs - first
     h_in = np.zeros((B * ns, in_stride), dtype=np.uint8)
     n_in = np.zeros(B * n_msgs, dtype=np.int32)
@@ -132,6 +126,45 @@ def test_split_messages_batch(dev, seed, in_stride):
                 assert np.array_equal(out[q, : mo[k].n], mo[k].buf[: mo[k].n]), (b, k)
             else:
                 assert src[q] == -1
+
+
+@pytest.mark.parametrize("seed,in_stride", [(0, 65536), (1, 65536), (2, 65536), (3, 65541), (4, 65664 + 56)])
+def test_split_messages_batch(dev, seed, in_stride):
+    """Landing slots on 128-B lines and off them (odd strides): the rows that
+    share a source line through LDS see every phase of it."""
+    rng = np.random.default_rng(7000 + seed)
+    n_msgs, first, buf_len = 128, 126, 65535
+    cases = [split_case(rng, n_msgs=n_msgs, first=first, buf_len=buf_len)[0] for _ in range(16)]
+    _split_batch_check(dev, cases, n_msgs, first, buf_len, in_stride)
+
+
+@pytest.mark.parametrize("in_stride", [65536, 65539])
+def test_split_messages_batch_gso_edges(dev, in_stride):
+    """gsoSize at the edges of the kernel's shared-line path (round 6: rows of
+    one message share 128-B source lines for 128 <= gsoSize <= 1,650, others
+    copy directly): 127 / 128 / 129, 1,649 / 1,650 / 1,651, 3,000, with short
+    tails and with several messages' packets in one 16-row block."""
+    rng = np.random.default_rng(7100 + in_stride)
+    n_msgs, first, buf_len = 128, 124, 65535
+    gs = (127, 128, 129, 1649, 1650, 1651, 3000, 1452)
+    cases = []
+    for b in range(12):
+        msgs = []
+        for s in range(n_msgs):
+            m = Msg(rng.integers(0, 256, buf_len, dtype=np.uint8))
+            m.addr = f"addr{s}"
+            msgs.append(m)
+        for s in range(first, n_msgs):
+            g = gs[(b * 4 + s) % len(gs)]
+            segs = int(rng.integers(1, max(2, min(40, 60000 // g))))
+            n = min(g * segs - int(rng.integers(0, g)), buf_len)
+            m = msgs[s]
+            m.n = max(n, 1)
+            ctl = gro_cmsg(g)
+            m.oob[: len(ctl)] = np.frombuffer(ctl, dtype=np.uint8)
+            m.nn = len(ctl)
+        cases.append(msgs)
+    _split_batch_check(dev, cases, n_msgs, first, buf_len, in_stride)
 
 
 @pytest.mark.parametrize("seed", range(3))
