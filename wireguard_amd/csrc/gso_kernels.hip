@@ -1019,13 +1019,13 @@ __device__ __forceinline__ uint4 lds16_a4(const uint8_t* p) {
   return make_uint4(q[0], q[1], q[2], q[3]);
 }
 
-template <int U, bool NT>
+template <int U, bool NT, int ROWS = 16>
 __device__ __forceinline__ void gso_rows_body(const uint8_t* arena, const wgcs_gso_job job, uint32_t jb, int by,
                                               int gy, uint32_t max_segs, uint8_t* out, uint32_t out_stride,
                                               bool has_pos, const GsoOutPos pos, uint32_t offset, uint32_t room,
                                               int32_t* sizes, int32_t* count, int32_t* status,
                                               const uint8_t* hlds = nullptr) {
-  constexpr int ROWS = 16;
+  static_assert(ROWS % 4 == 0, "4 rows per wave");  // ROWS = 4 x the workgroup's waves
 #ifdef WGCS_GSO_STAMPS  // timing-only build (scripts/probe_gso_stamps.py): s_memrealtime per wave phase
   uint64_t stp[5] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0};
 #endif
@@ -1380,9 +1380,15 @@ __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0,
         if (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) return 2;
         return 0;
       };
+      // workgroup 0 reads the inline payload too; the others need only the
+      // record and a virtio read's inline header (chunks < 64): their loads
+      // 1-2 point past the record and return zeros without a memory access
+      const int o1 = blockIdx.x == 0 ? 16 * (64 + lane) : 0x7FFFFFF0;
+      const int o2 = blockIdx.x == 0 ? 16 * (128 + lane) : 0x7FFFFFF0;
       auto poll = [&](u32x4s (&x)[3]) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) x[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * (64 * j + lane), 0, 17);
+        x[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 0, 17);  // sc0 sc1
+        x[1] = __builtin_amdgcn_raw_buffer_load_b128(rs, o1, 0, 17);
+        x[2] = __builtin_amdgcn_raw_buffer_load_b128(rs, o2, 0, 17);
       };
       // two polls in flight, issued half a round trip apart: a posted request
       // is seen ~RTT/4 sooner on average than with one poll at a time
@@ -1462,8 +1468,9 @@ __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0,
       const uint8_t* vb = gptr(kRqVbufLo, kRqVbufHi);
       // the inline header: vb[k] at LDS byte (vb & 15) + k
       const uint8_t* hl = w(kRqHdrInl) ? reinterpret_cast<const uint8_t*>(s_hdr) + ((uintptr_t)vb & 15u) : nullptr;
-      gso_rows_body<WGCS_GSO_U, false>(vb, job, 0, (int)blockIdx.x, (int)gridDim.x, kb, gptr(kRqOutLo, kRqOutHi), 0,
-                                       true, pos, 0, w(kRqRoom), h, h + kb, h + kb + 1, hl);
+      gso_rows_body<WGCS_GSO_U, false, 4 * kRingWaves>(vb, job, 0, (int)blockIdx.x, (int)gridDim.x, kb,
+                                                         gptr(kRqOutLo, kRqOutHi), 0, true, pos, 0, w(kRqRoom), h,
+                                                         h + kb, h + kb + 1, hl);
     }
     // completion: every wave's stores done; a request that stored results
     // releases them at system scope (the fence's own wait made explicit:
@@ -1508,7 +1515,7 @@ __global__ __launch_bounds__(256) void ring_kernel(RingCtl* ctl, uint32_t last0,
 
 hipError_t launch_ring(RingCtl* ctl, uint32_t nb, uint32_t last, uint64_t idle_ticks, hipStream_t s) {
   if (nb == 0 || nb > kRingMaxBlocks) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ring_kernel, dim3(nb), dim3(256), 0, s, ctl, last, idle_ticks);
+  hipLaunchKernelGGL(ring_kernel, dim3(nb), dim3(64 * kRingWaves), 0, s, ctl, last, idle_ticks);
   return hipGetLastError();
 }
 

@@ -43,7 +43,7 @@ struct wgcs_ring {
   size_t in_cap = 0;
   uint8_t* stage = nullptr;   // coherent pinned: segments / meta of a handleVirtioRead
   size_t stage_cap = 0;
-  uint32_t nb = 3;            // workgroups (segment groups of a 64-KiB read: 3 x 16 rows)
+  uint32_t nb = kRingBlocks;  // workgroups (segment groups of a 64-KiB read, kRingWaves x 4 rows each)
   uint64_t idle_ticks = 0;    // s_memrealtime ticks (100 MHz)
   uint32_t seq = 0;           // last request number posted
   uint64_t requests = 0, launches = 0;
